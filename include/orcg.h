@@ -1,0 +1,179 @@
+/*
+ * orcg.h — C ABI of the MI355X-native ORC column-stream decoder (liborcgpu).
+ *
+ * This is the drop-in boundary for the reference's stream-decoder hot path.
+ * Every entry point is plain C (pointers + sizes, no torch / HIP C++ types);
+ * hipStream_t travels as void*. The reference interfaces each group replaces
+ * are cited inline (paths relative to the apache/orc checkout). No exceptions
+ * cross this ABI: every call returns an ORCG_* status and the message is
+ * available from orcg_ctx_last_error() / orcg_*_last_error(). The C++ adapter
+ * (orc_amd/csrc/GpuRleDecoder.hh) rethrows them as orc::ParseError /
+ * orc::InvalidArgument with the reference's messages
+ * (c++/include/orc/Exceptions.hh:40-60); the JNI shim in INTEGRATION.md throws
+ * java.io.IOException.
+ *
+ * Memory ownership: the caller owns every src/dst buffer and
+ * the library never frees caller memory. Device scratch lives in an orcg_ctx,
+ * one per reader thread (reentrant; contexts are not shared between threads).
+ *
+ * Value semantics are those of orc::RleDecoderV2 (c++/src/RleDecoderV2.cc):
+ * zigzag for signed streams, int64 wraparound, static_cast narrowing for
+ * int32/int16 outputs, and null slots (not_null[i] == 0) left untouched.
+ */
+#ifndef ORCG_H
+#define ORCG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status ------------------------------------------------------------ */
+enum {
+  ORCG_OK = 0,
+  ORCG_PARSE_ERROR = 1,      /* orc::ParseError (corrupt / truncated stream) */
+  ORCG_INVALID_ARGUMENT = 2, /* orc::InvalidArgument (bad call, bad position) */
+  ORCG_DEVICE_ERROR = 3,     /* HIP runtime failure or no usable device */
+  ORCG_OUT_OF_MEMORY = 4
+};
+
+/* ---- context (one per reader thread) ------------------------------------ */
+typedef struct orcg_ctx orcg_ctx;
+
+/* Create a context bound to HIP device `device`, with its own non-blocking
+ * stream. Replaces nothing in the reference (the reference has no device);
+ * it is the owner of device scratch that MemoryPool (c++/include/orc/
+ * MemoryPool.hh:27-33) plays for host buffers. */
+int orcg_ctx_create(int device, orcg_ctx** out);
+void orcg_ctx_destroy(orcg_ctx* ctx);
+/* Use an external stream (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int orcg_ctx_set_stream(orcg_ctx* ctx, void* hip_stream);
+void* orcg_ctx_stream(orcg_ctx* ctx);
+/* Wait for the context stream and collect any device-side decode error of
+ * the launches issued since the last call (first error in value order). */
+int orcg_ctx_synchronize(orcg_ctx* ctx);
+const char* orcg_ctx_last_error(const orcg_ctx* ctx);
+
+const char* orcg_version(void);
+/* Number of visible HIP devices (0 when none; never aborts). */
+int orcg_device_count(void);
+
+/* ---- segments: the ORC-native parallel sync points ----------------------
+ * A segment is a run-aligned byte offset in an uncompressed (or already
+ * decompressed) stream plus the index of the first value of the run that
+ * starts there. Row-index positions (site/specification/ORCv1.md:1266-1272;
+ * recorded by RleEncoderV2::recordPosition) are exactly this: (byte offset of
+ * the run start, values of that run to skip). Segment k covers every run
+ * whose first byte lies in [segs[k].byte_offset, segs[k+1].byte_offset)
+ * (the last one runs to the end of the stream). */
+typedef struct orcg_segment {
+  uint64_t byte_offset;
+  uint64_t value_index;
+} orcg_segment;
+
+/* ---- RLEv2 integer streams ----------------------------------------------
+ * Replaces the run loop of orc::RleDecoderV2::next<T>
+ * (c++/src/RleDecoderV2.cc:132-453) and its bit unpackers
+ * BitUnpackDefault/BitUnpackAVX512::readLongs (c++/src/BpackingDefault.cc:
+ * 330-366, c++/src/BpackingAvx512.cc:2443-2586) for a whole stream or a
+ * row-group range at once. */
+
+/* Host run walk: reads only run headers (the host holds the bytes after
+ * decompression) and cuts the stream into segments of at most
+ * ~max_segment_bytes / max_segment_values. It also finds the first corrupt
+ * run, reported lazily by the decoders exactly where the reference would
+ * throw (RleDecoderV2.cc:38, :307, :328-330, :412-415). */
+typedef struct orcg_rlev2_plan orcg_rlev2_plan;
+int orcg_rlev2_plan_create(const uint8_t* src, uint64_t src_len, uint64_t max_segment_bytes,
+                           uint64_t max_segment_values, orcg_rlev2_plan** out);
+void orcg_rlev2_plan_destroy(orcg_rlev2_plan* plan);
+/* values decodable before the first corrupt run (all values if none) */
+uint64_t orcg_rlev2_plan_values(const orcg_rlev2_plan* plan);
+uint64_t orcg_rlev2_plan_segments(const orcg_rlev2_plan* plan, const orcg_segment** segs);
+/* ORCG_OK, or the status of the first corrupt run (*at_value = its first
+ * value index, *msg = the reference's ParseError text). */
+int orcg_rlev2_plan_error(const orcg_rlev2_plan* plan, uint64_t* at_value, const char** msg);
+
+/* Device-resident decode (asynchronous on the context stream).
+ * d_src: stream bytes in HBM; d_segs: segment table in HBM (nsegs entries);
+ * values with index v in [value_begin, value_begin + nvalues) are written
+ * dense to d_dst[v - value_begin] as int64/int32/int16 (dst_bytes 8/4/2).
+ * Corrupt runs set the context's device error record (see
+ * orcg_ctx_synchronize). */
+int orcg_rlev2_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                             const orcg_segment* d_segs, uint64_t nsegs, uint64_t value_begin,
+                             uint64_t nvalues, void* d_dst, int dst_bytes);
+
+/* Same, but the segment table is the column's ROW_INDEX positions as the
+ * writer records them: d_positions[2*g] = byte offset of the run holding row
+ * g*rows_per_group, d_positions[2*g+1] = values of that run to skip
+ * (ORCv1.md:1266-1272; RleDecoderV2::seek, RleDecoderV2.cc:109-117). The
+ * first value of segment g is g*rows_per_group - skip. No host work. */
+int orcg_rlev2_decode_positions_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len,
+                                       int is_signed, const uint64_t* d_positions,
+                                       uint64_t ngroups, uint64_t rows_per_group,
+                                       uint64_t value_begin, uint64_t nvalues, void* d_dst,
+                                       int dst_bytes);
+
+/* Host-buffer decode (the SURVEY.md §8b sketch): H2D, decode, D2H; with a
+ * not_null mask the n positions receive values in order and null slots are
+ * left untouched (RleDecoderV2::copyDataFromBuffer, :437-453). Synchronous. */
+int orcg_rlev2_decode_i64(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int is_signed,
+                          const char* not_null, uint64_t n, int64_t* dst);
+int orcg_rlev2_decode_i32(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int is_signed,
+                          const char* not_null, uint64_t n, int32_t* dst);
+int orcg_rlev2_decode_i16(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int is_signed,
+                          const char* not_null, uint64_t n, int16_t* dst);
+
+/* ---- stateful decoder: drop-in for orc::RleDecoder ----------------------
+ * Mirrors class RleDecoder (c++/src/RLE.hh:109-141) as created by
+ * createRleDecoder(stream, isSigned, RleVersion_2, pool, metrics)
+ * (c++/src/RLE.hh:163, c++/src/RLE.cc:48-60): the stream is bulk-decoded on
+ * the device on creation and next()/skip()/seek() serve slices, so run state
+ * persists across calls of any size and errors surface at the same value as
+ * in the reference. */
+typedef struct orcg_rle_decoder orcg_rle_decoder;
+int orcg_rle_decoder_create(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int is_signed,
+                            int rle_version, orcg_rle_decoder** out);
+void orcg_rle_decoder_destroy(orcg_rle_decoder* dec);
+int orcg_rle_decoder_next_i64(orcg_rle_decoder* dec, int64_t* data, uint64_t n, const char* not_null);
+int orcg_rle_decoder_next_i32(orcg_rle_decoder* dec, int32_t* data, uint64_t n, const char* not_null);
+int orcg_rle_decoder_next_i16(orcg_rle_decoder* dec, int16_t* data, uint64_t n, const char* not_null);
+/* RleDecoder::skip (RleDecoderV2.cc:119-130) */
+int orcg_rle_decoder_skip(orcg_rle_decoder* dec, uint64_t n);
+/* RleDecoder::seek(PositionProvider&) (RleDecoderV2.cc:109-117) for an
+ * uncompressed stream: positions = {byte offset, values to skip}. */
+int orcg_rle_decoder_seek(orcg_rle_decoder* dec, const uint64_t* positions, uint64_t npositions);
+/* Java face (java/core/src/java/org/apache/orc/impl/
+ * RunLengthIntegerReaderV2.java:371-396, nextVector): null slots get 1 and
+ * *is_repeating reports whether every slot holds the same value. is_null may
+ * be NULL (no nulls). */
+int orcg_rle_decoder_next_vector_java(orcg_rle_decoder* dec, int64_t* vector, const uint8_t* is_null,
+                                      uint64_t n, int* is_repeating);
+const char* orcg_rle_decoder_last_error(const orcg_rle_decoder* dec);
+
+/* ---- synthetic streams (writer side, for benchmarks and tests) ----------
+ * A minimal RLEv2 writer: DIRECT runs of up to 512 values at the smallest
+ * width from the 5-bit table (aligned = round the width up to the
+ * byte-aligned set, as RleEncoderV2's SPEED strategy does,
+ * c++/src/RleEncoderV2.cc). Optionally records row-index positions
+ * ({byte offset, values to skip} per rows_per_group) the way
+ * RleEncoderV2::recordPosition does. */
+int orcg_rlev2_encode_direct(const int64_t* values, uint64_t n, int is_signed, int aligned,
+                             uint8_t* dst, uint64_t dst_cap, uint64_t* out_len,
+                             uint64_t rows_per_group, uint64_t* positions);
+/* General run builder: run i encodes the next lengths[i] values with
+ * kinds[i] (0 SHORT_REPEAT, 1 DIRECT, 2 PATCHED_BASE, 3 DELTA); fails with
+ * ORCG_INVALID_ARGUMENT if the values are not representable that way.
+ * run_offsets (optional, nruns entries) receives each run's byte offset. */
+int orcg_rlev2_encode_runs(const int64_t* values, uint64_t n, int is_signed, const uint8_t* kinds,
+                           const uint32_t* lengths, uint64_t nruns, uint8_t* dst, uint64_t dst_cap,
+                           uint64_t* out_len, uint64_t* run_offsets);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORCG_H */

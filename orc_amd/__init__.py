@@ -1,0 +1,24 @@
+"""orc_amd — MI355X-native decoder for Apache ORC column streams.
+
+The hot path (RLEv2 integer streams; byte/boolean RLE; string-dictionary
+gather) runs as hand-written HIP kernels for gfx950 in liborcgpu.so, reached
+through the C ABI in include/orcg.h. This package is the thin host-side
+mirror of the reference's decoder interface (c++/src/RLE.hh) over that ABI.
+"""
+from ._lib import DeviceError, InvalidArgument, OrcError, ParseError  # noqa: F401
+from .rle import (  # noqa: F401
+    Context,
+    Plan,
+    RleDecoderV2,
+    RleVersion_1,
+    RleVersion_2,
+    create_rle_decoder,
+    decode_device,
+    decode_positions_device,
+    default_context,
+    encode_direct,
+    encode_runs,
+    rlev2_decode,
+)
+
+__version__ = "0.1.0"

@@ -1,0 +1,110 @@
+"""ctypes binding of liborcgpu.so (include/orcg.h).
+
+The product path has no CPU fallback: if the shared library is missing or no
+HIP device is usable, every decode raises instead of silently computing on
+the host.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liborcgpu.so")
+
+ORCG_OK = 0
+ORCG_PARSE_ERROR = 1
+ORCG_INVALID_ARGUMENT = 2
+ORCG_DEVICE_ERROR = 3
+ORCG_OUT_OF_MEMORY = 4
+
+
+class OrcError(RuntimeError):
+    status = None
+
+
+class ParseError(OrcError):
+    """orc::ParseError (c++/include/orc/Exceptions.hh:40)."""
+
+    status = ORCG_PARSE_ERROR
+
+
+class InvalidArgument(OrcError):
+    """orc::InvalidArgument (c++/include/orc/Exceptions.hh:52)."""
+
+    status = ORCG_INVALID_ARGUMENT
+
+
+class DeviceError(OrcError):
+    status = ORCG_DEVICE_ERROR
+
+
+_EXC = {ORCG_PARSE_ERROR: ParseError, ORCG_INVALID_ARGUMENT: InvalidArgument,
+        ORCG_DEVICE_ERROR: DeviceError, ORCG_OUT_OF_MEMORY: DeviceError}
+
+vp, u64, i32, sz, cp = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_size_t, ctypes.c_char_p
+
+# (name, argtypes, restype): every symbol include/orcg.h declares.
+SIGNATURES = [
+    ("orcg_ctx_create", [i32, ctypes.POINTER(vp)], i32),
+    ("orcg_ctx_destroy", [vp], None),
+    ("orcg_ctx_set_stream", [vp, vp], i32),
+    ("orcg_ctx_stream", [vp], vp),
+    ("orcg_ctx_synchronize", [vp], i32),
+    ("orcg_ctx_last_error", [vp], cp),
+    ("orcg_version", [], cp),
+    ("orcg_device_count", [], i32),
+    ("orcg_rlev2_plan_create", [vp, u64, u64, u64, ctypes.POINTER(vp)], i32),
+    ("orcg_rlev2_plan_destroy", [vp], None),
+    ("orcg_rlev2_plan_values", [vp], u64),
+    ("orcg_rlev2_plan_segments", [vp, ctypes.POINTER(vp)], u64),
+    ("orcg_rlev2_plan_error", [vp, ctypes.POINTER(u64), ctypes.POINTER(cp)], i32),
+    ("orcg_rlev2_decode_device", [vp, vp, u64, i32, vp, u64, u64, u64, vp, i32], i32),
+    ("orcg_rlev2_decode_positions_device", [vp, vp, u64, i32, vp, u64, u64, u64, u64, vp, i32], i32),
+    ("orcg_rlev2_decode_i64", [vp, vp, u64, i32, vp, u64, vp], i32),
+    ("orcg_rlev2_decode_i32", [vp, vp, u64, i32, vp, u64, vp], i32),
+    ("orcg_rlev2_decode_i16", [vp, vp, u64, i32, vp, u64, vp], i32),
+    ("orcg_rle_decoder_create", [vp, vp, u64, i32, i32, ctypes.POINTER(vp)], i32),
+    ("orcg_rle_decoder_destroy", [vp], None),
+    ("orcg_rle_decoder_next_i64", [vp, vp, u64, vp], i32),
+    ("orcg_rle_decoder_next_i32", [vp, vp, u64, vp], i32),
+    ("orcg_rle_decoder_next_i16", [vp, vp, u64, vp], i32),
+    ("orcg_rle_decoder_skip", [vp, u64], i32),
+    ("orcg_rle_decoder_seek", [vp, vp, u64], i32),
+    ("orcg_rle_decoder_next_vector_java", [vp, vp, vp, u64, ctypes.POINTER(i32)], i32),
+    ("orcg_rle_decoder_last_error", [vp], cp),
+    ("orcg_rlev2_encode_direct", [vp, u64, i32, i32, vp, u64, ctypes.POINTER(u64), u64, vp], i32),
+    ("orcg_rlev2_encode_runs", [vp, u64, i32, vp, vp, u64, vp, u64, ctypes.POINTER(u64), vp], i32),
+]
+
+_lib = None
+
+
+def load():
+    """Load liborcgpu.so (building it first if absent). torch is imported
+    first so that the library binds to the HIP runtime torch already loaded
+    (both carry SONAME libamdhip64.so.7)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (shares its libamdhip64 with us)
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        from . import build as _build
+        _build.build()
+    L = ctypes.CDLL(LIB_PATH)
+    for name, args, res in SIGNATURES:
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def check(rc, msg_fn=None):
+    if rc == ORCG_OK:
+        return
+    msg = msg_fn() if msg_fn else ""
+    if isinstance(msg, bytes):
+        msg = msg.decode(errors="replace")
+    raise _EXC.get(rc, OrcError)(msg or "orcg status %d" % rc)

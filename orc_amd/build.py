@@ -1,0 +1,51 @@
+"""Build liborcgpu.so in-tree with hipcc for gfx950 (no JIT cache: the .so
+travels to the GPU box with the repo snapshot)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "liborcgpu.so")
+OBJ = os.path.join(HERE, "build")
+ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["rlev2_kernels.hip", "orcg_api.cpp", "encoder.cpp"]
+HEADERS = ["orcg_internal.hh", os.path.join("..", "..", "include", "orcg.h")]
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value"]
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def build(force=False, verbose=False):
+    os.makedirs(OBJ, exist_ok=True)
+    hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
+    objs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJ, s + ".o")
+        objs.append(obj)
+        if not force and _mtime(obj) > max(_mtime(src), hdr_time):
+            continue
+        cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+        if s.endswith(".hip"):
+            cmd[1:1] = ["-x", "hip", "--offload-arch=" + ARCH]
+        else:
+            cmd[1:1] = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    if force or _mtime(OUT) < max(_mtime(o) for o in objs):
+        cmd = [HIPCC, "-shared", "-fPIC", "-o", OUT] + objs + ["-Wl,-soname,liborcgpu.so"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

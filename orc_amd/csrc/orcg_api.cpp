@@ -1,0 +1,526 @@
+// liborcgpu C ABI: contexts, the host run planner, host/device decode entry
+// points and the stateful drop-in decoder for orc::RleDecoder
+// (c++/src/RLE.hh:109-163). Kernels live in *_kernels.hip.
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "orcg_internal.hh"
+
+namespace orcg {
+
+const char* dev_error_message(uint32_t code) {
+  switch (code) {
+    case kErrBadRead: return "bad read in RleDecoderV2::readByte";
+    case kErrPatchedPl0: return "Corrupt PATCHED_BASE encoded data (pl==0)!";
+    case kErrPatchedWidth: return "Corrupt PATCHED_BASE encoded data (patchBitSize + pgw > 64)!";
+    case kErrDeltaLength: return "Illegal run length for delta encoding: 1";
+    case kErrBadSegment: return "Stream position is not at a run boundary";
+    case kErrByteBadRead: return "bad read in nextBuffer";
+    case kErrDictIndex: return "Entry index out of range in StringDictionaryColumn";
+  }
+  return "unknown device error";
+}
+
+int dev_error_status(uint32_t code) {
+  return code == kErrBadSegment ? ORCG_INVALID_ARGUMENT : ORCG_PARSE_ERROR;
+}
+
+int set_error(Ctx* ctx, int status, const std::string& msg) {
+  if (ctx) ctx->last_error = msg;
+  return status;
+}
+
+int hip_check(Ctx* ctx, hipError_t e, const char* what) {
+  if (e == hipSuccess) return ORCG_OK;
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return set_error(ctx, e == hipErrorOutOfMemory ? ORCG_OUT_OF_MEMORY : ORCG_DEVICE_ERROR, m);
+}
+
+int scratch(Ctx* ctx, int slot, size_t bytes, void** out) {
+  if (bytes == 0) bytes = 16;
+  if (ctx->scratch_cap[slot] < bytes) {
+    if (ctx->d_scratch[slot]) {
+      hipStreamSynchronize(ctx->stream);
+      hipFree(ctx->d_scratch[slot]);
+      ctx->d_scratch[slot] = nullptr;
+      ctx->scratch_cap[slot] = 0;
+    }
+    size_t cap = std::max(bytes, (size_t)1 << 20);
+    int rc = hip_check(ctx, hipMalloc(&ctx->d_scratch[slot], cap), "hipMalloc scratch");
+    if (rc) return rc;
+    ctx->scratch_cap[slot] = cap;
+  }
+  *out = ctx->d_scratch[slot];
+  return ORCG_OK;
+}
+
+// ------------------------------------------------------------------------
+// Host run walk. Header arithmetic identical to the device walk (and to
+// RleDecoderV2::next*, c++/src/RleDecoderV2.cc:184-435); only header bytes
+// are read. Errors are recorded with the first value index of the bad run.
+// ------------------------------------------------------------------------
+namespace {
+
+const uint8_t kFbs[32] = {1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16,
+                          17, 18, 19, 20, 21, 22, 23, 24, 26, 28, 30, 32, 40, 48, 56, 64};
+
+uint32_t closest_fixed_bits(uint32_t n) {
+  if (n == 0) return 1;
+  if (n <= 24) return n;
+  if (n <= 26) return 26;
+  if (n <= 28) return 28;
+  if (n <= 30) return 30;
+  if (n <= 32) return 32;
+  if (n <= 40) return 40;
+  if (n <= 48) return 48;
+  if (n <= 56) return 56;
+  return 64;
+}
+
+// Parses the run at `pos`. Returns kErrNone and sets run_len (values) and
+// run_end (bytes), or a DevErr.
+uint32_t parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_len,
+                   uint64_t* run_end) {
+  const uint32_t fb = s[pos];
+  const uint32_t kind = fb >> 6;
+  if (kind == 0) {
+    const uint32_t nb = ((fb >> 3) & 7) + 1;
+    *run_len = (fb & 7) + 3;
+    *run_end = pos + 1 + nb;
+    return *run_end > len ? kErrBadRead : kErrNone;
+  }
+  if (pos + 2 > len) return kErrBadRead;
+  const uint64_t L = ((uint64_t)(fb & 1) << 8 | s[pos + 1]) + 1;
+  *run_len = L;
+  if (kind == 1 || kind == 2) {
+    const uint32_t W = kFbs[(fb >> 1) & 0x1f];
+    uint64_t data = pos + 2;
+    uint32_t cfb = 0, pl = 0;
+    if (kind == 2) {
+      if (pos + 4 > len) return kErrBadRead;
+      const uint32_t third = s[pos + 2], fourth = s[pos + 3];
+      const uint32_t bw = (third >> 5) + 1;
+      const uint32_t pbs = kFbs[third & 0x1f];
+      const uint32_t pgw = (fourth >> 5) + 1;
+      pl = fourth & 0x1f;
+      if (pl == 0) return kErrPatchedPl0;
+      if (pos + 4 + bw > len) return kErrBadRead;
+      data = pos + 4 + bw;
+      if (data + (W * L + 7) / 8 > len) return kErrBadRead;
+      if (pbs + pgw > 64) return kErrPatchedWidth;
+      cfb = closest_fixed_bits(pbs + pgw);
+    }
+    *run_end = data + (W * L + 7) / 8 + ((uint64_t)cfb * pl + 7) / 8;
+    return *run_end > len ? kErrBadRead : kErrNone;
+  }
+  const uint32_t fbo = (fb >> 1) & 0x1f;
+  const uint32_t W = fbo ? kFbs[fbo] : 0;
+  uint64_t q = pos + 2;
+  for (int k = 0; k < 2; ++k) {
+    uint32_t b;
+    do {
+      if (q >= len) return kErrBadRead;
+      b = s[q++];
+    } while (b >= 0x80);
+  }
+  if (W != 0 && L < 2) return kErrDeltaLength;
+  *run_end = q + (W ? ((uint64_t)W * (L - 2) + 7) / 8 : 0);
+  return *run_end > len ? kErrBadRead : kErrNone;
+}
+
+}  // namespace
+}  // namespace orcg
+
+using namespace orcg;
+
+struct orcg_rlev2_plan {
+  std::vector<orcg_segment> segs;
+  uint64_t values = 0;
+  uint32_t err = kErrNone;
+  uint64_t err_at = 0;
+};
+
+static orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes,
+                                  uint64_t max_values) {
+  auto* p = new orcg_rlev2_plan();
+  uint64_t pos = 0, vi = 0;
+  uint64_t seg_b = 0, seg_v = 0;
+  bool open = false;
+  while (pos < len) {
+    uint64_t L = 0, end = 0;
+    const uint32_t e = parse_run(src, len, pos, &L, &end);
+    if (e != kErrNone) {
+      p->err = e;
+      p->err_at = vi;
+      break;
+    }
+    if (!open || pos - seg_b >= max_bytes || vi - seg_v >= max_values) {
+      p->segs.push_back({pos, vi});
+      seg_b = pos;
+      seg_v = vi;
+      open = true;
+    }
+    pos = end;
+    vi += L;
+  }
+  p->values = vi;
+  return p;
+}
+
+extern "C" {
+
+const char* orcg_version(void) { return "orcg 0.1.0 (gfx950)"; }
+
+int orcg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int orcg_ctx_create(int device, orcg_ctx** out) {
+  if (!out) return ORCG_INVALID_ARGUMENT;
+  *out = nullptr;
+  int n = orcg_device_count();
+  if (device < 0 || device >= n) return ORCG_DEVICE_ERROR;
+  auto* c = new orcg_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->d_err, sizeof(unsigned long long)) != hipSuccess ||
+      hipMemset(c->d_err, 0xff, sizeof(unsigned long long)) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess) {
+    delete c;
+    return ORCG_DEVICE_ERROR;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return ORCG_OK;
+}
+
+void orcg_ctx_destroy(orcg_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (int i = 0; i < 4; ++i)
+    if (c->d_scratch[i]) hipFree(c->d_scratch[i]);
+  if (c->h_pinned) hipHostFree(c->h_pinned);
+  if (c->d_err) hipFree(c->d_err);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+int orcg_ctx_set_stream(orcg_ctx* c, void* s) {
+  if (!c) return ORCG_INVALID_ARGUMENT;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return ORCG_OK;
+}
+
+void* orcg_ctx_stream(orcg_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+const char* orcg_ctx_last_error(const orcg_ctx* c) { return c ? c->last_error.c_str() : ""; }
+
+int orcg_ctx_synchronize(orcg_ctx* c) { return c ? sync_ctx(c) : ORCG_INVALID_ARGUMENT; }
+
+}  // extern "C"
+
+namespace orcg {
+int sync_ctx(Ctx* c) {
+  (void)hipSetDevice(c->device);
+  int rc = hip_check(c, hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  if (rc) return rc;
+  unsigned long long rec = kNoError;
+  rc = hip_check(c, hipMemcpy(&rec, c->d_err, sizeof rec, hipMemcpyDeviceToHost), "read error record");
+  if (rc) return rc;
+  if (rec == kNoError) return ORCG_OK;
+  const uint32_t code = (uint32_t)(rec & 0xff);
+  c->last_error_value = rec >> 8;
+  hipMemset(c->d_err, 0xff, sizeof rec);
+  return set_error(c, dev_error_status(code), dev_error_message(code));
+}
+}  // namespace orcg
+
+extern "C" {
+
+// ---- plan ----------------------------------------------------------------
+int orcg_rlev2_plan_create(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values,
+                           orcg_rlev2_plan** out) {
+  if (!out || (len && !src)) return ORCG_INVALID_ARGUMENT;
+  *out = make_plan(src, len, max_bytes ? max_bytes : (16u << 10), max_values ? max_values : 8192);
+  return ORCG_OK;
+}
+void orcg_rlev2_plan_destroy(orcg_rlev2_plan* p) { delete p; }
+uint64_t orcg_rlev2_plan_values(const orcg_rlev2_plan* p) { return p ? p->values : 0; }
+uint64_t orcg_rlev2_plan_segments(const orcg_rlev2_plan* p, const orcg_segment** segs) {
+  if (!p) return 0;
+  if (segs) *segs = p->segs.data();
+  return p->segs.size();
+}
+int orcg_rlev2_plan_error(const orcg_rlev2_plan* p, uint64_t* at, const char** msg) {
+  if (!p || p->err == kErrNone) return ORCG_OK;
+  if (at) *at = p->err_at;
+  if (msg) *msg = dev_error_message(p->err);
+  return dev_error_status(p->err);
+}
+
+// ---- device entry points ---------------------------------------------------
+int orcg_rlev2_decode_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                             const orcg_segment* d_segs, uint64_t nsegs, uint64_t value_begin,
+                             uint64_t nvalues, void* d_dst, int dst_bytes) {
+  if (!c || (nsegs && (!d_src || !d_segs)) || (nvalues && !d_dst)) return ORCG_INVALID_ARGUMENT;
+  hipSetDevice(c->device);
+  return launch_rlev2_decode(c, d_src, src_len, is_signed, (const uint64_t*)d_segs, nsegs, false, 0,
+                             value_begin, nvalues, d_dst, dst_bytes);
+}
+
+int orcg_rlev2_decode_positions_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_len,
+                                       int is_signed, const uint64_t* d_positions, uint64_t ngroups,
+                                       uint64_t rows_per_group, uint64_t value_begin,
+                                       uint64_t nvalues, void* d_dst, int dst_bytes) {
+  if (!c || (ngroups && (!d_src || !d_positions)) || (nvalues && !d_dst) || rows_per_group == 0)
+    return ORCG_INVALID_ARGUMENT;
+  hipSetDevice(c->device);
+  return launch_rlev2_decode(c, d_src, src_len, is_signed, d_positions, ngroups, true,
+                             rows_per_group, value_begin, nvalues, d_dst, dst_bytes);
+}
+
+}  // extern "C"
+
+// ---- host-buffer decode ----------------------------------------------------
+// Decodes the first `count` values of a host stream into host `out` (dense).
+static int decode_host_dense(Ctx* c, const uint8_t* src, uint64_t len, int is_signed,
+                             const orcg_rlev2_plan* plan, uint64_t count, void* out, int width) {
+  if (count == 0) return ORCG_OK;
+  hipSetDevice(c->device);
+  void *d_src, *d_seg, *d_out;
+  int rc = scratch(c, 0, len + 16, &d_src);
+  if (!rc) rc = scratch(c, 1, plan->segs.size() * sizeof(orcg_segment), &d_seg);
+  if (!rc) rc = scratch(c, 2, count * (size_t)width, &d_out);
+  if (rc) return rc;
+  rc = hip_check(c, hipMemcpyAsync(d_src, src, len, hipMemcpyHostToDevice, c->stream), "H2D stream");
+  if (!rc)
+    rc = hip_check(c, hipMemcpyAsync(d_seg, plan->segs.data(), plan->segs.size() * sizeof(orcg_segment),
+                                     hipMemcpyHostToDevice, c->stream),
+                   "H2D segments");
+  if (!rc)
+    rc = launch_rlev2_decode(c, (const uint8_t*)d_src, len, is_signed, (const uint64_t*)d_seg,
+                             plan->segs.size(), false, 0, 0, count, d_out, width);
+  if (!rc)
+    rc = hip_check(c, hipMemcpyAsync(out, d_out, count * (size_t)width, hipMemcpyDeviceToHost, c->stream),
+                   "D2H values");
+  if (!rc) rc = sync_ctx(c);
+  return rc;
+}
+
+template <typename T>
+static int decode_host(orcg_ctx* c, const uint8_t* src, uint64_t len, int is_signed,
+                       const char* not_null, uint64_t n, T* dst) {
+  if (!c || (len && !src) || (n && !dst)) return ORCG_INVALID_ARGUMENT;
+  uint64_t k = n;
+  if (not_null) {
+    k = 0;
+    for (uint64_t i = 0; i < n; ++i) k += not_null[i] ? 1 : 0;
+  }
+  std::unique_ptr<orcg_rlev2_plan> plan(make_plan(src, len, 16u << 10, 8192));
+  if (k > plan->values) {
+    const uint32_t e = plan->err != kErrNone ? plan->err : (uint32_t)kErrBadRead;
+    return set_error(c, dev_error_status(e), dev_error_message(e));
+  }
+  if (!not_null) return decode_host_dense(c, src, len, is_signed, plan.get(), k, dst, sizeof(T));
+  std::vector<T> dense(k);
+  int rc = decode_host_dense(c, src, len, is_signed, plan.get(), k, dense.data(), sizeof(T));
+  if (rc) return rc;
+  uint64_t j = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (not_null[i]) dst[i] = dense[j++];
+  return ORCG_OK;
+}
+
+extern "C" {
+int orcg_rlev2_decode_i64(orcg_ctx* c, const uint8_t* s, uint64_t l, int sg, const char* nn, uint64_t n,
+                          int64_t* d) {
+  return decode_host(c, s, l, sg, nn, n, d);
+}
+int orcg_rlev2_decode_i32(orcg_ctx* c, const uint8_t* s, uint64_t l, int sg, const char* nn, uint64_t n,
+                          int32_t* d) {
+  return decode_host(c, s, l, sg, nn, n, d);
+}
+int orcg_rlev2_decode_i16(orcg_ctx* c, const uint8_t* s, uint64_t l, int sg, const char* nn, uint64_t n,
+                          int16_t* d) {
+  return decode_host(c, s, l, sg, nn, n, d);
+}
+}  // extern "C"
+
+// ---- stateful decoder ----------------------------------------------------------
+struct orcg_rle_decoder {
+  Ctx* ctx = nullptr;
+  int is_signed = 0;
+  std::vector<uint8_t> src;
+  std::unique_ptr<orcg_rlev2_plan> plan;
+  uint64_t origin = 0;          // byte offset the decoded values start at
+  std::vector<int64_t> values;  // dense decoded values from `origin`
+  uint64_t cursor = 0;
+  std::string last_error;
+
+  int fail(int status, const std::string& m) {
+    last_error = m;
+    return status;
+  }
+  // (Re)decode the stream suffix starting at byte `from`.
+  int load_from(uint64_t from) {
+    origin = from;
+    cursor = 0;
+    const uint8_t* s = src.data() + from;
+    const uint64_t len = src.size() - from;
+    plan.reset(make_plan(s, len, 16u << 10, 8192));
+    values.assign(plan->values, 0);
+    int rc = decode_host_dense(ctx, s, len, is_signed, plan.get(), plan->values, values.data(), 8);
+    if (rc) return fail(rc, ctx->last_error);
+    return ORCG_OK;
+  }
+  int need(uint64_t k) {
+    if (cursor + k <= values.size()) return ORCG_OK;
+    const uint32_t e = plan->err != kErrNone ? plan->err : (uint32_t)kErrBadRead;
+    return fail(dev_error_status(e), dev_error_message(e));
+  }
+  template <typename T>
+  int next(T* data, uint64_t n, const char* nn) {
+    if (n && !data) return fail(ORCG_INVALID_ARGUMENT, "null data");
+    uint64_t k = n;
+    if (nn) {
+      k = 0;
+      for (uint64_t i = 0; i < n; ++i) k += nn[i] ? 1 : 0;
+    }
+    // values up to the failing run are delivered before the error, like the
+    // reference's partially filled batch
+    const uint64_t avail = std::min<uint64_t>(k, values.size() - cursor);
+    uint64_t j = 0;
+    for (uint64_t i = 0; i < n && j < avail; ++i) {
+      if (nn && !nn[i]) continue;
+      data[i] = (T)values[cursor + j++];
+    }
+    if (avail < k) {
+      cursor += avail;
+      return need(k - avail);
+    }
+    cursor += k;
+    return ORCG_OK;
+  }
+};
+
+extern "C" {
+
+int orcg_rle_decoder_create(orcg_ctx* c, const uint8_t* src, uint64_t len, int is_signed,
+                            int version, orcg_rle_decoder** out) {
+  if (!c || !out || (len && !src)) return ORCG_INVALID_ARGUMENT;
+  *out = nullptr;
+  if (version != 2)
+    return set_error(c, ORCG_INVALID_ARGUMENT, "only RleVersion_2 streams decode on the GPU");
+  auto* d = new orcg_rle_decoder();
+  d->ctx = c;
+  d->is_signed = is_signed;
+  d->src.assign(src, src + len);
+  int rc = d->load_from(0);
+  if (rc) {
+    c->last_error = d->last_error;
+    delete d;
+    return rc;
+  }
+  *out = d;
+  return ORCG_OK;
+}
+
+void orcg_rle_decoder_destroy(orcg_rle_decoder* d) { delete d; }
+
+int orcg_rle_decoder_next_i64(orcg_rle_decoder* d, int64_t* data, uint64_t n, const char* nn) {
+  return d ? d->next(data, n, nn) : ORCG_INVALID_ARGUMENT;
+}
+int orcg_rle_decoder_next_i32(orcg_rle_decoder* d, int32_t* data, uint64_t n, const char* nn) {
+  return d ? d->next(data, n, nn) : ORCG_INVALID_ARGUMENT;
+}
+int orcg_rle_decoder_next_i16(orcg_rle_decoder* d, int16_t* data, uint64_t n, const char* nn) {
+  return d ? d->next(data, n, nn) : ORCG_INVALID_ARGUMENT;
+}
+
+int orcg_rle_decoder_skip(orcg_rle_decoder* d, uint64_t n) {
+  if (!d) return ORCG_INVALID_ARGUMENT;
+  const uint64_t avail = std::min<uint64_t>(n, d->values.size() - d->cursor);
+  d->cursor += avail;
+  return avail < n ? d->need(n - avail) : ORCG_OK;
+}
+
+int orcg_rle_decoder_seek(orcg_rle_decoder* d, const uint64_t* pos, uint64_t npos) {
+  if (!d) return ORCG_INVALID_ARGUMENT;
+  if (!pos || npos < 2) return d->fail(ORCG_INVALID_ARGUMENT, "uncompressed RLE position needs 2 values");
+  const uint64_t byte = pos[0], skip = pos[1];
+  if (byte > d->src.size()) return d->fail(ORCG_INVALID_ARGUMENT, "Seek past end of stream");
+  // Is `byte` a run start of the current decoding? Walk run headers from the
+  // nearest segment cut (host bytes; cheap).
+  bool found = false;
+  uint64_t vi = 0;
+  if (byte >= d->origin) {
+    const uint64_t rel = byte - d->origin;
+    const auto& segs = d->plan->segs;
+    auto it = std::upper_bound(segs.begin(), segs.end(), rel,
+                               [](uint64_t b, const orcg_segment& s) { return b < s.byte_offset; });
+    if (it != segs.begin()) {
+      --it;
+      uint64_t p = it->byte_offset, v = it->value_index;
+      const uint8_t* s = d->src.data() + d->origin;
+      const uint64_t len = d->src.size() - d->origin;
+      while (p < rel && p < len) {
+        uint64_t L, end;
+        if (parse_run(s, len, p, &L, &end) != kErrNone) break;
+        p = end;
+        v += L;
+      }
+      if (p == rel && v <= d->values.size()) {
+        found = true;
+        vi = v;
+      }
+    }
+  }
+  if (found) {
+    d->cursor = vi;
+  } else {
+    int rc = d->load_from(byte);
+    if (rc) return rc;
+  }
+  return orcg_rle_decoder_skip(d, skip);
+}
+
+int orcg_rle_decoder_next_vector_java(orcg_rle_decoder* d, int64_t* vector, const uint8_t* is_null,
+                                      uint64_t n, int* is_repeating) {
+  if (!d || (n && !vector) || !is_repeating) return ORCG_INVALID_ARGUMENT;
+  // RunLengthIntegerReaderV2.nextVector (RunLengthIntegerReaderV2.java:371-396)
+  if (*is_repeating && is_null && n > 0 && is_null[0]) return ORCG_OK;
+  if (is_null) {
+    std::vector<char> nn(n);
+    for (uint64_t i = 0; i < n; ++i) nn[i] = is_null[i] ? 0 : 1;
+    int rc = d->next(vector, n, nn.data());
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+      if (is_null[i]) vector[i] = 1;
+  } else {
+    int rc = d->next(vector, n, nullptr);
+    if (rc) return rc;
+  }
+  bool rep = true;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (rep && i > 0 &&
+        (vector[0] != vector[i] || (is_null ? is_null[0] != is_null[i] : false)))
+      rep = false;
+  }
+  *is_repeating = rep ? 1 : 0;
+  return ORCG_OK;
+}
+
+const char* orcg_rle_decoder_last_error(const orcg_rle_decoder* d) {
+  return d ? d->last_error.c_str() : "";
+}
+
+}  // extern "C"

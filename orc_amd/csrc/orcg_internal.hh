@@ -1,0 +1,62 @@
+// Internal declarations shared by the liborcgpu translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/orcg.h"
+
+namespace orcg {
+
+// Device-side error codes (the low byte of the packed device error record).
+// Messages are the reference's ParseError texts (c++/src/RleDecoderV2.cc).
+enum DevErr : uint32_t {
+  kErrNone = 0,
+  kErrBadRead = 1,         // "bad read in RleDecoderV2::readByte"            :38
+  kErrPatchedPl0 = 2,      // "Corrupt PATCHED_BASE encoded data (pl==0)!"     :307
+  kErrPatchedWidth = 3,    // "... (patchBitSize + pgw > 64)!"                 :328-330
+  kErrDeltaLength = 4,     // "Illegal run length for delta encoding: 1"       :412-415
+  kErrBadSegment = 5,      // positions / segment table not run aligned (InvalidArgument)
+  kErrByteBadRead = 6,     // "bad read in nextBuffer" (ByteRLE.cc:364)
+  kErrDictIndex = 7,       // "Entry index out of range in StringDictionaryColumn" (ColumnReader.cc:578)
+};
+
+const char* dev_error_message(uint32_t code);
+int dev_error_status(uint32_t code);
+
+// The device error record: min over (value_index << 8 | code). ~0 = none.
+constexpr unsigned long long kNoError = ~0ull;
+
+struct Ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  unsigned long long* d_err = nullptr;  // device error record
+  std::string last_error;
+  uint64_t last_error_value = 0;
+  // grow-only device scratch
+  void* d_scratch[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t scratch_cap[4] = {0, 0, 0, 0};
+  void* h_pinned = nullptr;
+  size_t pinned_cap = 0;
+};
+
+int set_error(Ctx* ctx, int status, const std::string& msg);
+int hip_check(Ctx* ctx, hipError_t e, const char* what);
+int scratch(Ctx* ctx, int slot, size_t bytes, void** out);
+// Wait for the context stream and fold the device error record into a status.
+int sync_ctx(Ctx* ctx);
+
+// Kernel launchers (rlev2_kernels.hip). segtab is either orcg_segment[] or the
+// row-index positions array (positions_mode, with rows_per_group).
+int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
+                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
+                        void* d_dst, int dst_bytes);
+
+}  // namespace orcg
+
+struct orcg_ctx : orcg::Ctx {};

@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU-box session: each GPU step has its own time limit; a fault, abort,
+# segfault or timeout stops the session (no further GPU work in this call).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+: > $OUT/status.log
+run() {
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] start $name" >> $OUT/status.log
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >> $OUT/status.log
+  case $rc in 124|137|134|139) echo "fatal rc=$rc in $name, stopping" >> $OUT/status.log; exit $rc;; esac
+  return 0
+}
+STEPS="${*:-pytest smoke bench prof}"
+for s in $STEPS; do
+  case $s in
+    info) run info 60 bash -c "rocm-smi --showproductname; nproc; lscpu | grep 'Model name'" ;;
+    pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    pytestcpu) run pytest_cpu 600 python -m pytest tests -m "not gpu" -q ;;
+    smoke) run smoke 300 python __graft_entry__.py smoke ;;
+    bench) run bench 600 python bench.py ;;
+    prof)
+      export TMPDIR=/tmp
+      run prof 600 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-verify ;;
+    pmc)
+      export TMPDIR=/tmp
+      run pmc_fetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$PWD/$OUT/pmc_fetch" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-verify
+      run pmc_write 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$PWD/$OUT/pmc_write" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-verify ;;
+    *) echo "unknown step $s" >> $OUT/status.log ;;
+  esac
+done
+echo done >> $OUT/status.log

@@ -1,0 +1,190 @@
+"""GPU parity tests: the HIP RLEv2 decoder (through the C ABI) against the
+reference's known answers and the CPU oracle. Bit-exact throughout.
+
+Needs a real MI355X: run with `pytest -m gpu`.
+"""
+import numpy as np
+import pytest
+
+from conftest import assert_matches, decode_batches, load_golden
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+RLEV2 = load_golden("kat_rlev2.json")
+
+
+@pytest.fixture(scope="module")
+def orc():
+    import orc_amd
+
+    ctx = orc_amd.default_context(0)
+    assert ctx is not None
+    return orc_amd
+
+
+@pytest.mark.parametrize("fx", RLEV2, ids=[f["name"] for f in RLEV2])
+def test_kat_stateful(orc, fx):
+    """Same reads as the reference test: batches 1, 3, 7 and all at once,
+    with its notNull mask (c++/test/TestRleDecoder.cc)."""
+    data = bytes.fromhex(fx["data"])
+    nn = fx.get("not_null")
+    for b in fx["batches"]:
+        dec = orc.create_rle_decoder(data, fx["signed"])
+        got = decode_batches(dec.next, fx["expected"], b, nn)
+        assert_matches(fx["expected"], got, nn, "%s batch=%s" % (fx["name"], b))
+    if "seek" in fx:
+        dec = orc.create_rle_decoder(data, fx["signed"])
+        dec.seek(*fx["seek"]["position"])
+        got = list(dec.next(3)) + list(dec.next(3)) + list(dec.next(1))
+        assert got == fx["seek"]["expected"]
+
+
+@pytest.mark.parametrize("fx", RLEV2, ids=[f["name"] for f in RLEV2])
+def test_kat_narrow_matches_oracle(orc, fx):
+    data = bytes.fromhex(fx["data"])
+    nn = fx.get("not_null")
+    n = len(fx["expected"])
+    nnarr = None if nn is None else np.array(nn, dtype=np.uint8)
+    for dt in (np.int64, np.int32, np.int16):
+        want = oracle.RleDecoderV2(data, fx["signed"]).next(n, nnarr, dtype=dt)
+        got = orc.rlev2_decode(data, n, fx["signed"], not_null=nnarr, dtype=dt)
+        keep = np.ones(n, bool) if nn is None else nnarr.astype(bool)
+        np.testing.assert_array_equal(got[keep], want[keep])
+
+
+def _mixed(rng, signed, nruns):
+    from test_host_cpu import _mixed_stream
+
+    return _mixed_stream(rng, signed, nruns)
+
+
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("signed", [True, False])
+def test_mixed_runs_vs_oracle(orc, seed, signed):
+    rng = np.random.default_rng(100 + seed)
+    for _ in range(20):
+        v, kinds, lens = _mixed(rng, signed, 300)
+        try:
+            data, _ = orc.encode_runs(v, signed, kinds, lens)
+            break
+        except orc.OrcError:
+            continue
+    want = oracle.rlev2_decode(data.tobytes(), v.size, signed)
+    np.testing.assert_array_equal(want, v)
+    got = orc.rlev2_decode(data.tobytes(), v.size, signed)
+    np.testing.assert_array_equal(got, want)
+    # batched reads with a random null mask through the stateful decoder
+    nn = (rng.random(v.size + v.size // 3) > 0.25).astype(np.uint8)
+    nn[np.cumsum(nn) > v.size] = 0
+    nd = nn.size
+    odec = oracle.RleDecoderV2(data.tobytes(), signed)
+    gdec = orc.create_rle_decoder(data.tobytes(), signed)
+    i = 0
+    while i < nd:
+        k = int(min(rng.integers(1, 2000), nd - i))
+        w = odec.next(k, nn[i:i + k])
+        g = gdec.next(k, nn[i:i + k])
+        m = nn[i:i + k].astype(bool)
+        np.testing.assert_array_equal(g[m], w[m])
+        i += k
+
+
+@pytest.mark.parametrize("bits", [1, 2, 3, 4, 5, 7, 8, 11, 13, 16, 17, 24, 26, 28, 30, 32, 40, 48, 56, 64])
+@pytest.mark.parametrize("signed", [True, False])
+def test_direct_every_width(orc, bits, signed):
+    rng = np.random.default_rng(bits)
+    n = 70001
+    if bits == 64:
+        v = rng.integers(-(1 << 63), (1 << 63) - 1, size=n, dtype=np.int64, endpoint=True)
+    elif signed:
+        v = rng.integers(-(1 << (bits - 1)), (1 << (bits - 1)), size=n, dtype=np.int64)
+    else:
+        v = rng.integers(0, (1 << bits) - 1, size=n, dtype=np.int64, endpoint=True)
+    for aligned in (False, True):
+        data, _ = orc.encode_direct(v, signed, aligned=aligned)
+        got = orc.rlev2_decode(data.tobytes(), n, signed)
+        np.testing.assert_array_equal(got, v)
+
+
+def test_device_positions_decode_and_subranges(orc):
+    import torch
+
+    rng = np.random.default_rng(7)
+    n, stride = 1_000_003, 10_000
+    v = rng.integers(-(1 << 40), 1 << 40, size=n, dtype=np.int64)
+    data, pos = orc.encode_direct(v, True, aligned=True, rows_per_group=stride)
+    ctx = orc.default_context(0)
+    d_src = torch.from_numpy(data).cuda()
+    d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+    out = torch.empty(n, dtype=torch.int64, device="cuda")
+    orc.decode_positions_device(ctx, d_src, d_pos, stride, n, True, out)
+    ctx.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), v)
+    # row range [a, b) as RowReaderOptions::range would request
+    for a, b in [(0, 1), (12345, 54321), (n - 7, n), (9_999, 10_001)]:
+        o2 = torch.zeros(b - a, dtype=torch.int64, device="cuda")
+        orc.decode_positions_device(ctx, d_src, d_pos, stride, b - a, True, o2, value_begin=a)
+        ctx.synchronize()
+        np.testing.assert_array_equal(o2.cpu().numpy(), v[a:b])
+    # int32 narrowing on device
+    o3 = torch.empty(n, dtype=torch.int32, device="cuda")
+    orc.decode_positions_device(ctx, d_src, d_pos, stride, n, True, o3)
+    ctx.synchronize()
+    np.testing.assert_array_equal(o3.cpu().numpy(), v.astype(np.int32))
+
+
+def test_device_segments_mixed(orc):
+    import torch
+
+    rng = np.random.default_rng(11)
+    v, kinds, lens = _mixed(rng, True, 2000)
+    data, offs = orc.encode_runs(v, True, kinds, lens)
+    plan = orc.Plan(data.tobytes(), max_segment_bytes=1024, max_segment_values=1000)
+    segs = plan.segments()
+    ctx = orc.default_context(0)
+    out = torch.empty(v.size, dtype=torch.int64, device="cuda")
+    orc.decode_device(ctx, torch.from_numpy(data).cuda(), torch.from_numpy(segs.view(np.int64)).cuda(),
+                      v.size, True, out)
+    ctx.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), v)
+
+
+@pytest.mark.parametrize("case", ["pl0", "pgw", "delta_len", "truncated"])
+def test_errors_match_reference(orc, case):
+    good, _ = orc.encode_direct(np.arange(700, dtype=np.int64), False)
+    g = good.tobytes()
+    tail = {
+        "pl0": bytes([0x8E, 0x09, 0x2B, 0x20, 0x07, 0xD0]),
+        "pgw": bytes([0x8E, 0x09, 0x3F, 0xE1, 0x07]) + bytes(64),  # pw 64 + pgw 8 > 64
+        "delta_len": bytes([0xC2, 0x00, 0x02, 0x02]),
+        "truncated": bytes([0x5E, 0x03, 0x5C]),
+    }[case]
+    data = g + tail
+    # values before the corrupt run decode fine, the next read raises the
+    # reference's message (RleDecoderV2.cc:38, :307, :328-330, :412-415)
+    with pytest.raises(oracle.OracleError) as want:
+        oracle.RleDecoderV2(data, False).next(701)
+    dec = orc.create_rle_decoder(data, False)
+    np.testing.assert_array_equal(dec.next(700), np.arange(700))
+    with pytest.raises(orc.ParseError) as got:
+        dec.next(1)
+    assert str(got.value) == str(want.value)
+
+
+def test_large_roundtrip_property(orc):
+    """Full-range int64 at 2e7 rows: decode(encode(v)) == v (size-independent
+    round-trip property; the oracle is checked on the small cases)."""
+    import torch
+
+    n = 20_000_000
+    g = torch.Generator(device="cuda").manual_seed(42)
+    v = torch.randint(-(1 << 63), (1 << 63) - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+    vh = v.cpu().numpy()
+    data, pos = orc.encode_direct(vh, True, aligned=True, rows_per_group=10_000)
+    ctx = orc.default_context(0)
+    out = torch.empty_like(v)
+    orc.decode_positions_device(ctx, torch.from_numpy(data).cuda(), torch.from_numpy(pos.view(np.int64)).cuda(),
+                                10_000, n, True, out)
+    ctx.synchronize()
+    assert torch.equal(out, v)
