@@ -57,6 +57,13 @@ void* orcg_ctx_stream(orcg_ctx* ctx);
 int orcg_ctx_synchronize(orcg_ctx* ctx);
 const char* orcg_ctx_last_error(const orcg_ctx* ctx);
 
+/* Kernel selection for RLEv2 decode (tuning / A-B measurement). TILED (the
+ * default) stages segment chunks through LDS by LDS-DMA and walks headers in
+ * LDS; WAVE_WALK is one wavefront per segment reading HBM directly. Both are
+ * bit-identical. */
+enum { ORCG_RLEV2_TILED = 0, ORCG_RLEV2_WAVE_WALK = 1 };
+int orcg_ctx_set_rlev2_variant(orcg_ctx* ctx, int variant);
+
 const char* orcg_version(void);
 /* Number of visible HIP devices (0 when none; never aborts). */
 int orcg_device_count(void);

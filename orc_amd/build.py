@@ -10,8 +10,8 @@ OUT = os.path.join(HERE, "liborcgpu.so")
 OBJ = os.path.join(HERE, "build")
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rlev2_kernels.hip", "orcg_api.cpp", "encoder.cpp"]
-HEADERS = ["orcg_internal.hh", os.path.join("..", "..", "include", "orcg.h")]
+SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "orcg_api.cpp", "encoder.cpp"]
+HEADERS = ["orcg_internal.hh", "rlev2_device.hh", os.path.join("..", "..", "include", "orcg.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value"]

@@ -220,6 +220,12 @@ int orcg_ctx_set_stream(orcg_ctx* c, void* s) {
   return ORCG_OK;
 }
 
+int orcg_ctx_set_rlev2_variant(orcg_ctx* c, int v) {
+  if (!c || (v != ORCG_RLEV2_TILED && v != ORCG_RLEV2_WAVE_WALK)) return ORCG_INVALID_ARGUMENT;
+  c->rlev2_variant = v;
+  return ORCG_OK;
+}
+
 void* orcg_ctx_stream(orcg_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 const char* orcg_ctx_last_error(const orcg_ctx* c) { return c ? c->last_error.c_str() : ""; }
@@ -273,7 +279,7 @@ int orcg_rlev2_decode_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_len
                              uint64_t nvalues, void* d_dst, int dst_bytes) {
   if (!c || (nsegs && (!d_src || !d_segs)) || (nvalues && !d_dst)) return ORCG_INVALID_ARGUMENT;
   hipSetDevice(c->device);
-  return launch_rlev2_decode(c, d_src, src_len, is_signed, (const uint64_t*)d_segs, nsegs, false, 0,
+  return launch_rlev2(c, d_src, src_len, is_signed, (const uint64_t*)d_segs, nsegs, false, 0,
                              value_begin, nvalues, d_dst, dst_bytes);
 }
 
@@ -284,7 +290,7 @@ int orcg_rlev2_decode_positions_device(orcg_ctx* c, const uint8_t* d_src, uint64
   if (!c || (ngroups && (!d_src || !d_positions)) || (nvalues && !d_dst) || rows_per_group == 0)
     return ORCG_INVALID_ARGUMENT;
   hipSetDevice(c->device);
-  return launch_rlev2_decode(c, d_src, src_len, is_signed, d_positions, ngroups, true,
+  return launch_rlev2(c, d_src, src_len, is_signed, d_positions, ngroups, true,
                              rows_per_group, value_begin, nvalues, d_dst, dst_bytes);
 }
 
@@ -307,7 +313,7 @@ static int decode_host_dense(Ctx* c, const uint8_t* src, uint64_t len, int is_si
                                      hipMemcpyHostToDevice, c->stream),
                    "H2D segments");
   if (!rc)
-    rc = launch_rlev2_decode(c, (const uint8_t*)d_src, len, is_signed, (const uint64_t*)d_seg,
+    rc = launch_rlev2(c, (const uint8_t*)d_src, len, is_signed, (const uint64_t*)d_seg,
                              plan->segs.size(), false, 0, 0, count, d_out, width);
   if (!rc)
     rc = hip_check(c, hipMemcpyAsync(out, d_out, count * (size_t)width, hipMemcpyDeviceToHost, c->stream),

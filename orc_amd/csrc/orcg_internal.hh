@@ -42,6 +42,7 @@ struct Ctx {
   size_t scratch_cap[4] = {0, 0, 0, 0};
   void* h_pinned = nullptr;
   size_t pinned_cap = 0;
+  int rlev2_variant = ORCG_RLEV2_TILED;  // which RLEv2 kernel to launch
 };
 
 int set_error(Ctx* ctx, int status, const std::string& msg);
@@ -56,6 +57,23 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                         uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
                         void* d_dst, int dst_bytes);
+
+int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                       const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
+                       uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
+                       void* d_dst, int dst_bytes);
+
+// Dispatch on ctx->rlev2_variant.
+inline int launch_rlev2(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
+                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
+                        void* d_dst, int dst_bytes) {
+  if (ctx->rlev2_variant == ORCG_RLEV2_WAVE_WALK)
+    return launch_rlev2_decode(ctx, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode,
+                               rows_per_group, value_begin, nvalues, d_dst, dst_bytes);
+  return launch_rlev2_tiled(ctx, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode,
+                            rows_per_group, value_begin, nvalues, d_dst, dst_bytes);
+}
 
 }  // namespace orcg
 

@@ -143,8 +143,11 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
   win.base = 0xffffffffu;
   win.word = 0;
 
+  bool patch_lds_clean = false;  // zeroed lazily on the first PATCHED_BASE run
   uint64_t pos = seg_start;
-  while (pos < seg_end) {
+  // Values past the output range are never needed: stop there, so corrupt
+  // runs beyond it are not reported (the reference throws lazily too).
+  while (pos < seg_end && vi < value_end) {
     const uint32_t rel = (uint32_t)(pos - bias);
     if (win.base == 0xffffffffu || rel < win.base || rel + 32 > win.base + 256) {
       win.base = rel & ~3u;
@@ -221,6 +224,12 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
           }
           const uint64_t pmask = (1ull << pbs) - 1;  // pbs <= 63 here
           const uint32_t e_lo = (uint32_t)entry, e_hi = (uint32_t)(entry >> 32);
+          if (!patch_lds_clean) {
+#pragma unroll
+            for (int i = 0; i < 512 / kWave; ++i) patch_lds[i * kWave + lane] = 0;
+            __syncthreads();
+            patch_lds_clean = true;
+          }
           for (int pass = 0; pass < 2; ++pass) {  // pass 0: scatter, pass 1: clear
             uint64_t cum = 0, prev = 0;
             bool first = true;
@@ -351,7 +360,7 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
     pos = run_end;
     vi += L;
   }
-  if (v_next != ~0ull && vi != v_next) report(err, vi, kErrBadSegment);
+  if (v_next != ~0ull && vi < value_end && vi != v_next) report(err, vi, kErrBadSegment);
 }
 
 }  // namespace

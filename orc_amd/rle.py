@@ -51,6 +51,10 @@ class Context:
         raw = getattr(stream, "cuda_stream", stream)
         check(self._L.orcg_ctx_set_stream(self._h, ctypes.c_void_p(raw)))
 
+    def set_rlev2_variant(self, variant):
+        """0 = tiled LDS kernel (default), 1 = one-wave-per-segment walk."""
+        check(self._L.orcg_ctx_set_rlev2_variant(self._h, int(variant)))
+
     def synchronize(self):
         check(self._L.orcg_ctx_synchronize(self._h), self.last_error)
 

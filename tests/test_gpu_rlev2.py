@@ -14,13 +14,16 @@ pytestmark = pytest.mark.gpu
 RLEV2 = load_golden("kat_rlev2.json")
 
 
-@pytest.fixture(scope="module")
-def orc():
+@pytest.fixture(scope="module", params=[0, 1], ids=["tiled", "wavewalk"])
+def orc(request):
+    """Every parity test runs against both RLEv2 kernels (ORCG_RLEV2_TILED,
+    ORCG_RLEV2_WAVE_WALK)."""
     import orc_amd
 
     ctx = orc_amd.default_context(0)
-    assert ctx is not None
-    return orc_amd
+    ctx.set_rlev2_variant(request.param)
+    yield orc_amd
+    ctx.set_rlev2_variant(0)
 
 
 @pytest.mark.parametrize("fx", RLEV2, ids=[f["name"] for f in RLEV2])
