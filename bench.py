@@ -94,6 +94,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--variant", type=int, default=0, help="0 tiled (default), 1 wave-walk")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,6 +119,7 @@ def main():
 
     stream = torch.cuda.Stream()
     ctx = orc_amd.Context(local_rank, stream=stream)
+    ctx.set_rlev2_variant(args.variant)
     with torch.cuda.stream(stream):
         d_src = torch.from_numpy(data).to("cuda")
         d_pos = torch.from_numpy(pos.view(np.int64)).to("cuda")
@@ -186,6 +188,7 @@ def main():
                 "stream_bytes": S,
                 "row_index_stride": args.stride,
                 "parallelism": "stripe-sharded x%d" % world,
+                "kernel": ["rlev2_tiled_kernel", "rlev2_decode_kernel"][args.variant],
             },
             "roofline": {
                 "bound": "hbm",

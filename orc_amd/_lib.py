@@ -72,6 +72,7 @@ SIGNATURES = [
     ("orcg_rle_decoder_seek", [vp, vp, u64], i32),
     ("orcg_rle_decoder_next_vector_java", [vp, vp, vp, u64, ctypes.POINTER(i32)], i32),
     ("orcg_rle_decoder_last_error", [vp], cp),
+    ("orcg_probe_copy", [vp, vp, vp, u64, i32], i32),
     ("orcg_rlev2_encode_direct", [vp, u64, i32, i32, vp, u64, ctypes.POINTER(u64), u64, vp], i32),
     ("orcg_rlev2_encode_runs", [vp, u64, i32, vp, vp, u64, vp, u64, ctypes.POINTER(u64), vp], i32),
 ]

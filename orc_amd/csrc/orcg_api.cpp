@@ -221,7 +221,8 @@ int orcg_ctx_set_stream(orcg_ctx* c, void* s) {
 }
 
 int orcg_ctx_set_rlev2_variant(orcg_ctx* c, int v) {
-  if (!c || (v != ORCG_RLEV2_TILED && v != ORCG_RLEV2_WAVE_WALK)) return ORCG_INVALID_ARGUMENT;
+  // 0 tiled (default), 1 wave-walk; 2..6 are tiled tuning experiments
+  if (!c || v < 0 || v > 9) return ORCG_INVALID_ARGUMENT;
   c->rlev2_variant = v;
   return ORCG_OK;
 }

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of the RLEv2 kernel variants in ONE process (guide rule:
+perf deltas come from interleaved rounds), next to a device copy of the same
+byte count as the roofline reference. Prints one JSON line per variant."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--bits", type=int, default=64)
+    ap.add_argument("--variants", default="0,1,2,3,4,5,6")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--stride", type=int, default=10_000)
+    args = ap.parse_args()
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(42)
+    n = args.rows
+    if args.bits == 64:
+        v = rng.integers(-(1 << 63), (1 << 63) - 1, size=n, dtype=np.int64, endpoint=True)
+    else:
+        v = rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=n, dtype=np.int64)
+    data, pos = orc_amd.encode_direct(v, True, aligned=True, rows_per_group=args.stride)
+    S = data.size
+    stream = torch.cuda.Stream()
+    ctx = orc_amd.Context(0, stream=stream)
+    with torch.cuda.stream(stream):
+        d_src = torch.from_numpy(data).cuda()
+        d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+        d_out = torch.empty(n, dtype=torch.int64, device="cuda")
+        d_vals = torch.from_numpy(v).cuda()
+        d_copy = torch.empty_like(d_vals)
+    stream.synchronize()
+    variants = [int(x) for x in args.variants.split(",")]
+
+    L = orc_amd._lib.load()
+
+    def run(var):
+        if var == "copy":
+            with torch.cuda.stream(stream):
+                d_copy.copy_(d_vals)
+        elif isinstance(var, str) and var.startswith("probe"):
+            orc_amd._lib.check(L.orcg_probe_copy(ctx.handle, orc_amd.rle._tensor_ptr(d_vals),
+                                                 orc_amd.rle._tensor_ptr(d_copy), 8 * n, int(var[5:])))
+        else:
+            ctx.set_rlev2_variant(var)
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, args.stride, n, True, d_out)
+
+    # verify every variant once
+    for var in variants:
+        d_out.zero_()
+        run(var)
+        ctx.synchronize()
+        assert torch.equal(d_out, d_vals), "variant %d mismatch" % var
+    refs = ["copy", "probe0", "probe1", "probe2", "probe3"]
+    times = {var: [] for var in refs + variants}
+    for _ in range(args.rounds):
+        for var in refs + variants:
+            for _ in range(2):
+                run(var)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(args.iters):
+                run(var)
+            e1.record(stream)
+            e1.synchronize()
+            times[var].append(e0.elapsed_time(e1) / args.iters)
+    for var, ts in times.items():
+        ms = float(np.median(ts))
+        byts = 16 * n if isinstance(var, str) else S + 8 * n
+        print(json.dumps({"variant": var, "bits": args.bits, "ms_median": round(ms, 4),
+                          "ms_min": round(float(np.min(ts)), 4),
+                          "GBps": round(byts / ms / 1e6, 1), "bytes": int(byts)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

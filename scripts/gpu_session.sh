@@ -23,6 +23,9 @@ for s in $STEPS; do
     pytestcpu) run pytest_cpu 600 python -m pytest tests -m "not gpu" -q ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py ;;
+    ab) run ab 600 python scripts/ab_rlev2.py --variants 0,5,6,7,8,9 ;;
+    ab13) run ab13 600 python scripts/ab_rlev2.py --bits 13 --variants 0,5,6,7,8,9 ;;
+    benchwalk) run bench_walk 600 python bench.py --variant 1 --no-cpu-baseline ;;
     prof)
       export TMPDIR=/tmp
       run prof 600 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-verify ;;
