@@ -162,6 +162,64 @@ int orcg_rle_decoder_next_vector_java(orcg_rle_decoder* dec, int64_t* vector, co
                                       uint64_t n, int* is_repeating);
 const char* orcg_rle_decoder_last_error(const orcg_rle_decoder* dec);
 
+/* ---- byte RLE / boolean RLE (PRESENT, BOOLEAN, BYTE streams) -------------
+ * Replaces ByteRleDecoderImpl / BooleanRleDecoderImpl (c++/src/ByteRLE.hh:
+ * 71-126, ByteRLE.cc:359-643). Segments index decoded BYTES; byte-RLE
+ * row-index positions are (byte offset, bytes to skip) and boolean ones add
+ * the bits consumed of the next byte (ByteRLE.cc:409-417, :549-560). The
+ * plan accessors above (orcg_rlev2_plan_*) apply to byte plans too. */
+int orcg_byterle_plan_create(const uint8_t* src, uint64_t src_len, uint64_t max_segment_bytes,
+                             uint64_t max_segment_values, orcg_rlev2_plan** out);
+/* decoded bytes [value_begin, value_begin + nvalues) -> d_dst */
+int orcg_byterle_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len,
+                               const orcg_segment* d_segs, uint64_t nsegs, uint64_t value_begin,
+                               uint64_t nvalues, uint8_t* d_dst);
+/* rows (bits, MSB first) [row_begin, row_begin + nrows) -> one char 0/1 per row */
+int orcg_boolrle_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len,
+                               const orcg_segment* d_segs, uint64_t nsegs, uint64_t row_begin,
+                               uint64_t nrows, uint8_t* d_dst);
+
+/* Stateful drop-in for orc::ByteRleDecoder as created by
+ * createByteRleDecoder / createBooleanRleDecoder (c++/src/ByteRLE.hh:114,126):
+ * next(data, n, notNull) leaves null slots untouched (byte) or writes 0
+ * (boolean); seek takes 2 (byte) or 3 (boolean) position values. */
+typedef struct orcg_byte_rle_decoder orcg_byte_rle_decoder;
+int orcg_byte_rle_decoder_create(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int boolean,
+                                 orcg_byte_rle_decoder** out);
+void orcg_byte_rle_decoder_destroy(orcg_byte_rle_decoder* dec);
+int orcg_byte_rle_decoder_next(orcg_byte_rle_decoder* dec, char* data, uint64_t n, const char* not_null);
+int orcg_byte_rle_decoder_skip(orcg_byte_rle_decoder* dec, uint64_t n);
+int orcg_byte_rle_decoder_seek(orcg_byte_rle_decoder* dec, const uint64_t* positions, uint64_t npositions);
+const char* orcg_byte_rle_decoder_last_error(const orcg_byte_rle_decoder* dec);
+
+/* ---- nullable columns and string dictionaries ----------------------------
+ * Null scatter (RleDecoderV2::copyDataFromBuffer with notNull,
+ * RleDecoderV2.cc:437-453): dense values -> the non-null rows of d_out
+ * (width 8/4/2/1 bytes). fill_nulls = 0 leaves null slots untouched (C++);
+ * 1 writes fill_value there (Java's 1, RunLengthIntegerReaderV2.java:371-396). */
+int orcg_scatter_not_null_device(orcg_ctx* ctx, const void* d_dense, const uint8_t* d_not_null,
+                                 uint64_t n, void* d_out, int width, int fill_nulls,
+                                 int64_t fill_value);
+/* Dictionary LENGTH values -> offsets[dict_size + 1] (loadStringDictionary,
+ * c++/src/DictionaryLoader.cc:69-80). */
+int orcg_dict_offsets_device(orcg_ctx* ctx, const int64_t* d_lengths, uint64_t dict_size,
+                             int64_t* d_offsets);
+/* Per non-null row: start = offsets[idx], length = offsets[idx+1] -
+ * offsets[idx]; idx >= dict_size raises "Entry index out of range in
+ * StringDictionaryColumn" (StringDictionaryColumnReader::next,
+ * c++/src/ColumnReader.cc:561-594). Starts are blob-relative: the C++ adapter
+ * adds the host blob base after D2H. index_width 8 or 4. */
+int orcg_dict_gather_device(orcg_ctx* ctx, const void* d_indices, int index_width,
+                            const uint8_t* d_not_null, uint64_t n, const int64_t* d_offsets,
+                            uint64_t dict_size, int64_t* d_start, int64_t* d_length);
+/* IntegerColumnReader<LongVectorBatch>::next for a whole stripe column
+ * (c++/src/ColumnReader.cc:81-104, 224-258): PRESENT (boolean RLE; NULL/0 if
+ * the column has no nulls) + DATA (RLEv2) host streams -> not_null[n] and
+ * data[n] with null slots untouched. */
+int orcg_decode_integer_column(orcg_ctx* ctx, const uint8_t* present, uint64_t present_len,
+                               const uint8_t* data, uint64_t data_len, int is_signed, uint64_t n,
+                               int64_t* out, char* not_null);
+
 /* ---- synthetic streams (writer side, for benchmarks and tests) ----------
  * A minimal RLEv2 writer: DIRECT runs of up to 512 values at the smallest
  * width from the 5-bit table (aligned = round the width up to the

@@ -7,18 +7,27 @@ mirror of the reference's decoder interface (c++/src/RLE.hh) over that ABI.
 """
 from ._lib import DeviceError, InvalidArgument, OrcError, ParseError  # noqa: F401
 from .rle import (  # noqa: F401
+    BytePlan,
+    ByteRleDecoder,
     Context,
     Plan,
     RleDecoderV2,
     RleVersion_1,
     RleVersion_2,
+    byterle_decode_device,
+    create_boolean_rle_decoder,
+    create_byte_rle_decoder,
     create_rle_decoder,
+    decode_integer_column,
+    dict_gather_device,
+    dict_offsets_device,
     decode_device,
     decode_positions_device,
     default_context,
     encode_direct,
     encode_runs,
     rlev2_decode,
+    scatter_not_null_device,
 )
 
 __version__ = "0.1.0"

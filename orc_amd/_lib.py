@@ -72,6 +72,19 @@ SIGNATURES = [
     ("orcg_rle_decoder_seek", [vp, vp, u64], i32),
     ("orcg_rle_decoder_next_vector_java", [vp, vp, vp, u64, ctypes.POINTER(i32)], i32),
     ("orcg_rle_decoder_last_error", [vp], cp),
+    ("orcg_byterle_plan_create", [vp, u64, u64, u64, ctypes.POINTER(vp)], i32),
+    ("orcg_byterle_decode_device", [vp, vp, u64, vp, u64, u64, u64, vp], i32),
+    ("orcg_boolrle_decode_device", [vp, vp, u64, vp, u64, u64, u64, vp], i32),
+    ("orcg_byte_rle_decoder_create", [vp, vp, u64, i32, ctypes.POINTER(vp)], i32),
+    ("orcg_byte_rle_decoder_destroy", [vp], None),
+    ("orcg_byte_rle_decoder_next", [vp, vp, u64, vp], i32),
+    ("orcg_byte_rle_decoder_skip", [vp, u64], i32),
+    ("orcg_byte_rle_decoder_seek", [vp, vp, u64], i32),
+    ("orcg_byte_rle_decoder_last_error", [vp], cp),
+    ("orcg_scatter_not_null_device", [vp, vp, vp, u64, vp, i32, i32, ctypes.c_int64], i32),
+    ("orcg_dict_offsets_device", [vp, vp, u64, vp], i32),
+    ("orcg_dict_gather_device", [vp, vp, i32, vp, u64, vp, u64, vp, vp], i32),
+    ("orcg_decode_integer_column", [vp, vp, u64, vp, u64, i32, u64, vp, vp], i32),
     ("orcg_probe_copy", [vp, vp, vp, u64, i32], i32),
     ("orcg_rlev2_encode_direct", [vp, u64, i32, i32, vp, u64, ctypes.POINTER(u64), u64, vp], i32),
     ("orcg_rlev2_encode_runs", [vp, u64, i32, vp, vp, u64, vp, u64, ctypes.POINTER(u64), vp], i32),

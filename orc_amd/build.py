@@ -10,7 +10,7 @@ OUT = os.path.join(HERE, "liborcgpu.so")
 OBJ = os.path.join(HERE, "build")
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "orcg_api.cpp", "encoder.cpp"]
+SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "byterle_kernels.hip", "column_kernels.hip", "orcg_api.cpp", "byterle_api.cpp", "encoder.cpp"]
 HEADERS = ["orcg_internal.hh", "rlev2_device.hh", os.path.join("..", "..", "include", "orcg.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

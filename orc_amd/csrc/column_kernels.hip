@@ -1,0 +1,208 @@
+// Column-level kernels around the stream decoders:
+//  * null scatter: dense decoded values -> row positions of a nullable column
+//    (RleDecoderV2::copyDataFromBuffer with notNull, c++/src/RleDecoderV2.cc:
+//    437-453; ColumnReader::next's PRESENT handling, c++/src/ColumnReader.cc:
+//    81-104). C++ leaves null slots untouched; the Java face writes 1
+//    (java/core/.../RunLengthIntegerReaderV2.java:371-396).
+//  * dictionary offsets: lengths -> exclusive prefix sum
+//    (loadStringDictionary, c++/src/DictionaryLoader.cc:69-80).
+//  * dictionary gather: index -> (blob offset, length) with the reference's
+//    bounds check (StringDictionaryColumnReader::next, c++/src/
+//    ColumnReader.cc:561-594).
+#include "rlev2_device.hh"
+
+namespace orcg {
+namespace {
+using namespace dev;
+
+constexpr int kTile = 4096;  // rows per scatter tile (256 threads x 16 rows)
+constexpr int kThreads = 256;
+
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t nn_bytes_count(u4 v) {
+  // each byte is 0 or non-zero; count non-zero bytes
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t x = v[k];
+    c += ((x & 0xffu) != 0) + ((x & 0xff00u) != 0) + ((x & 0xff0000u) != 0) + ((x & 0xff000000u) != 0);
+  }
+  return c;
+}
+
+__device__ __forceinline__ u4 load16(const uint8_t* nn, uint64_t row0, uint64_t n) {
+  if (row0 + 16 <= n && (((uintptr_t)(nn + row0)) & 15u) == 0) return *(const u4*)(nn + row0);
+  u4 v = {0, 0, 0, 0};
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (row0 + k < n) v[k >> 2] |= (uint32_t)nn[row0 + k] << (8 * (k & 3));
+  return v;
+}
+
+__global__ __launch_bounds__(kThreads) void tile_count_kernel(const uint8_t* __restrict__ nn, uint64_t n,
+                                                               uint32_t* __restrict__ counts) {
+  __shared__ uint32_t red[kThreads / kWave];
+  const uint64_t row0 = (uint64_t)blockIdx.x * kTile + threadIdx.x * 16u;
+  uint32_t c = row0 < n ? nn_bytes_count(load16(nn, row0, n)) : 0;
+  for (int d = kWave / 2; d > 0; d >>= 1) c += __shfl_down(c, d, kWave);
+  if ((threadIdx.x % kWave) == 0) red[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kThreads / kWave; ++w) t += red[w];
+    counts[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of `n` uint32 counts into uint64 offsets, one workgroup.
+__global__ __launch_bounds__(1024) void scan_kernel(const uint32_t* __restrict__ counts, uint64_t n,
+                                                     uint64_t* __restrict__ offsets) {
+  __shared__ uint64_t wsum[1024 / kWave];
+  __shared__ uint64_t carry_s;
+  const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (uint64_t b = 0; b < n; b += 1024) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t x = i < n ? counts[i] : 0;
+    const uint64_t inc = wave_inclusive_scan(x, lane);
+    if (lane == kWave - 1) wsum[wv] = inc;
+    __syncthreads();
+    uint64_t before = carry_s;
+    for (int w = 0; w < wv; ++w) before += wsum[w];
+    if (i < n) offsets[i] = before + inc - x;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry_s = before + inc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) offsets[n] = carry_s;
+}
+
+template <typename T, bool kFill>
+__global__ __launch_bounds__(kThreads) void scatter_kernel(const T* __restrict__ dense, const uint8_t* __restrict__ nn,
+                                                            uint64_t n, const uint64_t* __restrict__ tile_off,
+                                                            T* __restrict__ out, T fill) {
+  __shared__ uint32_t wsum[kThreads / kWave];
+  const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
+  const uint64_t row0 = (uint64_t)blockIdx.x * kTile + threadIdx.x * 16u;
+  const u4 v = row0 < n ? load16(nn, row0, n) : u4{0, 0, 0, 0};
+  const uint32_t c = nn_bytes_count(v);
+  uint32_t inc = c;
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += y;
+  }
+  if (lane == kWave - 1) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int w = 0; w < wv; ++w) before += wsum[w];
+  uint64_t rank = tile_off[blockIdx.x] + before + inc - c;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t r = row0 + k;
+    if (r < n) {
+      if ((v[k >> 2] >> (8 * (k & 3))) & 0xffu) out[r] = dense[rank++];
+      else if (kFill) out[r] = fill;
+    }
+  }
+}
+
+template <typename T>
+__global__ void dict_gather_kernel(const T* __restrict__ idx, const uint8_t* __restrict__ nn, uint64_t n,
+                                   const int64_t* __restrict__ offsets, uint64_t dict_size,
+                                   int64_t* __restrict__ out_start, int64_t* __restrict__ out_len,
+                                   unsigned long long* err) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (nn && !nn[i]) continue;
+    const uint64_t e = (uint64_t)(int64_t)idx[i];
+    if (e >= dict_size) {
+      report(err, i, kErrDictIndex);
+      continue;
+    }
+    const int64_t s = offsets[e];
+    out_start[i] = s;
+    out_len[i] = offsets[e + 1] - s;
+  }
+}
+
+__global__ __launch_bounds__(1024) void lengths_scan_kernel(const int64_t* __restrict__ lengths, uint64_t n,
+                                                             int64_t* __restrict__ offsets) {
+  __shared__ uint64_t wsum[1024 / kWave];
+  __shared__ uint64_t carry_s;
+  const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (uint64_t b = 0; b < n; b += 1024) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t x = i < n ? (uint64_t)lengths[i] : 0;
+    const uint64_t inc = wave_inclusive_scan(x, lane);
+    if (lane == kWave - 1) wsum[wv] = inc;
+    __syncthreads();
+    uint64_t before = carry_s;
+    for (int w = 0; w < wv; ++w) before += wsum[w];
+    if (i < n) offsets[i] = (int64_t)(before + inc - x);
+    __syncthreads();
+    if (threadIdx.x == 1023) carry_s = before + inc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) offsets[n] = (int64_t)carry_s;
+}
+
+}  // namespace
+
+int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,
+                   int fill_mode, int64_t fill) {
+  if (n == 0) return ORCG_OK;
+  const uint64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many rows");
+  void *d_counts, *d_off;
+  int rc = scratch(ctx, 5, tiles * sizeof(uint32_t), &d_counts);
+  if (!rc) rc = scratch(ctx, 6, (tiles + 1) * sizeof(uint64_t), &d_off);
+  if (rc) return rc;
+  hipLaunchKernelGGL(tile_count_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_nn, n,
+                     (uint32_t*)d_counts);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const uint32_t*)d_counts, tiles,
+                     (uint64_t*)d_off);
+#define ORCG_SC(T)                                                                                     \
+  do {                                                                                                 \
+    if (fill_mode)                                                                                     \
+      hipLaunchKernelGGL((scatter_kernel<T, true>), dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, \
+                         (const T*)d_dense, d_nn, n, (const uint64_t*)d_off, (T*)d_out, (T)fill);      \
+    else                                                                                               \
+      hipLaunchKernelGGL((scatter_kernel<T, false>), dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, \
+                         (const T*)d_dense, d_nn, n, (const uint64_t*)d_off, (T*)d_out, (T)fill);      \
+  } while (0)
+  switch (width) {
+    case 8: ORCG_SC(int64_t); break;
+    case 4: ORCG_SC(int32_t); break;
+    case 2: ORCG_SC(int16_t); break;
+    case 1: ORCG_SC(int8_t); break;
+    default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "width must be 8, 4, 2 or 1");
+  }
+#undef ORCG_SC
+  return hip_check(ctx, hipGetLastError(), "scatter launch");
+}
+
+int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets) {
+  hipLaunchKernelGGL(lengths_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, d_lengths, dict_size, d_offsets);
+  return hip_check(ctx, hipGetLastError(), "dictionary offsets launch");
+}
+
+int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t* d_nn, uint64_t n,
+                       const int64_t* d_offsets, uint64_t dict_size, int64_t* d_start, int64_t* d_len) {
+  if (n == 0) return ORCG_OK;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256 * 16);
+  if (idx_width == 8)
+    hipLaunchKernelGGL(dict_gather_kernel<int64_t>, dim3(grid), dim3(256), 0, ctx->stream, (const int64_t*)d_idx,
+                       d_nn, n, d_offsets, dict_size, d_start, d_len, ctx->d_err);
+  else if (idx_width == 4)
+    hipLaunchKernelGGL(dict_gather_kernel<int32_t>, dim3(grid), dim3(256), 0, ctx->stream, (const int32_t*)d_idx,
+                       d_nn, n, d_offsets, dict_size, d_start, d_len, ctx->d_err);
+  else
+    return set_error(ctx, ORCG_INVALID_ARGUMENT, "index width must be 8 or 4");
+  return hip_check(ctx, hipGetLastError(), "dictionary gather launch");
+}
+
+}  // namespace orcg

@@ -138,14 +138,8 @@ uint32_t parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_l
 
 using namespace orcg;
 
-struct orcg_rlev2_plan {
-  std::vector<orcg_segment> segs;
-  uint64_t values = 0;
-  uint32_t err = kErrNone;
-  uint64_t err_at = 0;
-};
 
-static orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes,
+orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes,
                                   uint64_t max_values) {
   auto* p = new orcg_rlev2_plan();
   uint64_t pos = 0, vi = 0;
@@ -206,7 +200,7 @@ void orcg_ctx_destroy(orcg_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 8; ++i)
     if (c->d_scratch[i]) hipFree(c->d_scratch[i]);
   if (c->h_pinned) hipHostFree(c->h_pinned);
   if (c->d_err) hipFree(c->d_err);
@@ -299,7 +293,7 @@ int orcg_rlev2_decode_positions_device(orcg_ctx* c, const uint8_t* d_src, uint64
 
 // ---- host-buffer decode ----------------------------------------------------
 // Decodes the first `count` values of a host stream into host `out` (dense).
-static int decode_host_dense(Ctx* c, const uint8_t* src, uint64_t len, int is_signed,
+int decode_host_dense(Ctx* c, const uint8_t* src, uint64_t len, int is_signed,
                              const orcg_rlev2_plan* plan, uint64_t count, void* out, int width) {
   if (count == 0) return ORCG_OK;
   hipSetDevice(c->device);

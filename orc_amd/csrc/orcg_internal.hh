@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -38,8 +39,10 @@ struct Ctx {
   std::string last_error;
   uint64_t last_error_value = 0;
   // grow-only device scratch
-  void* d_scratch[4] = {nullptr, nullptr, nullptr, nullptr};
-  size_t scratch_cap[4] = {0, 0, 0, 0};
+  // scratch slots: 0 stream, 1 segments, 2 dense values, 3 not-null,
+  // 4 column output, 5 tile counts, 6 tile offsets, 7 misc
+  void* d_scratch[8] = {};
+  size_t scratch_cap[8] = {};
   void* h_pinned = nullptr;
   size_t pinned_cap = 0;
   int rlev2_variant = ORCG_RLEV2_TILED;  // which RLEv2 kernel to launch
@@ -63,6 +66,14 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
                        void* d_dst, int dst_bytes);
 
+int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
+                   bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst);
+int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,
+                   int fill_mode, int64_t fill);
+int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets);
+int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t* d_nn, uint64_t n,
+                       const int64_t* d_offsets, uint64_t dict_size, int64_t* d_start, int64_t* d_len);
+
 // Dispatch on ctx->rlev2_variant.
 inline int launch_rlev2(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
@@ -78,3 +89,18 @@ inline int launch_rlev2(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
 }  // namespace orcg
 
 struct orcg_ctx : orcg::Ctx {};
+
+// Host run walk result (RLEv2 or byte RLE): segment cuts, decodable values,
+// first corrupt run.
+struct orcg_rlev2_plan {
+  std::vector<orcg_segment> segs;
+  uint64_t values = 0;
+  uint32_t err = orcg::kErrNone;
+  uint64_t err_at = 0;
+};
+
+orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
+orcg_rlev2_plan* make_byte_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
+// H2D + RLEv2 decode of the first `count` values + D2H into host `out`.
+int decode_host_dense(orcg::Ctx* c, const uint8_t* src, uint64_t len, int is_signed,
+                      const orcg_rlev2_plan* plan, uint64_t count, void* out, int width);

@@ -56,11 +56,38 @@ __device__ __forceinline__ u32x3 lds12(const uint32_t* w, uint32_t o) {
   return r;
 }
 
+// Run headers are parsed from a 256-byte slice of the LDS window held one
+// dword per lane and read back with v_readlane: one LDS round trip per slice
+// instead of one per header byte. kHdrLim bounds how far a header may reach
+// (DELTA's two varints take <= 22 bytes; longer ones are corrupt).
+constexpr uint32_t kHdrLim = 64;
+
+struct LaneWin {
+  uint32_t word = 0, base = 0xffffffffu;
+  __device__ __forceinline__ void load(const uint32_t* win, uint32_t hoff, uint32_t nwords, int lane) {
+    base = hoff & ~3u;
+    uint32_t idx = (base >> 2) + (uint32_t)lane;
+    if (idx >= nwords) idx = nwords - 1;
+    word = win[idx];
+  }
+  // make sure [hoff, hoff + kHdrLim) is inside the slice
+  __device__ __forceinline__ void cover(const uint32_t* win, uint32_t hoff, uint32_t nwords, int lane) {
+    if (base == 0xffffffffu || hoff < base || hoff + kHdrLim > base + 256) load(win, hoff, nwords, lane);
+  }
+  __device__ __forceinline__ uint32_t byte(uint32_t o) const {
+    o -= base;
+    return (rdlane(word, o >> 2) >> ((o & 3u) * 8)) & 0xffu;
+  }
+};
+
 // Expand one run (already validated by the walk) with one wave.
 template <int kOpt, typename T>
-__device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t hoff, uint64_t v0, int is_signed,
-                                           uint64_t value_begin, uint64_t value_end, T* dst, int lane) {
-  const Run r = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kMaxRun, is_signed);
+__device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords, uint32_t hoff, uint64_t v0,
+                                           int is_signed, uint64_t value_begin, uint64_t value_end, T* dst,
+                                           int lane) {
+  LaneWin hw;
+  hw.load(win, hoff, nwords, lane);
+  const Run r = parse_run([&](uint32_t i) { return hw.byte(hoff + i); }, ~0ull, kHdrLim, is_signed);
   const uint32_t L = r.L;
   if (v0 + L <= value_begin || v0 >= value_end) return;  // outside the requested rows
   const uint32_t d = hoff + r.data;  // LDS offset of the packed data
@@ -198,10 +225,12 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
   constexpr uint32_t kChunk = kWin - kMaxRun;
   uint64_t p = pos, v = vi;
   uint32_t n = 0, stop = 0;
+  LaneWin hw;
   while (p < seg_end && v < value_end && n < (uint32_t)kMaxRuns) {
     const uint32_t lp = (uint32_t)(p - wpos);
     if (lp >= kChunk && n > 0) break;  // starts in the next window
-    const Run r = parse_run([&](uint32_t i) { return lds_byte(win, lp + i); }, src_len - p, kMaxRun, is_signed);
+    hw.cover(win, lp, kWin / 4 + 8, lane);
+    const Run r = parse_run([&](uint32_t i) { return hw.byte(lp + i); }, src_len - p, kHdrLim, is_signed);
     uint32_t e = r.err;
     if (e == kErrNone && p + r.bytes > seg_end) e = kErrBadSegment;
     if (e == kErrNone && lp + r.bytes > lim) e = kErrBadRead;  // only a corrupt varint gets here
@@ -315,7 +344,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       const uint32_t n = s_ctl[0][0], stop = s_ctl[0][1];
       const uint64_t next_pos = pos + s_ctl[0][2], next_vi = vi + s_ctl[0][3];
       for (uint32_t k = wave; k < n; k += kWaves)
-        expand_run<kOpt>(s_win[0], s_off[0][k], vi + s_val[0][k], is_signed, value_begin, value_end, dst, lane);
+        expand_run<kOpt>(s_win[0], kWin / 4 + 8, s_off[0][k], vi + s_val[0][k], is_signed, value_begin, value_end, dst, lane);
       __syncthreads();  // the window is refilled next
       if (stop) return;
       pos = next_pos;
@@ -359,7 +388,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         }
       } else {
         for (uint32_t k = wave - 1; k < n; k += kWaves - 1)
-          expand_run<kOpt>(s_win[b], s_off[b][k], vi + s_val[b][k], is_signed, value_begin, value_end, dst,
+          expand_run<kOpt>(s_win[b], kWin / 4 + 8, s_off[b][k], vi + s_val[b][k], is_signed, value_begin, value_end, dst,
                            lane);
       }
       lds_barrier();

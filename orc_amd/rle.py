@@ -260,3 +260,117 @@ def encode_runs(values, is_signed, kinds, lengths):
                                    _ptr(dst), cap, ctypes.byref(out_len), _ptr(offs)),
           lambda: b"values not representable with the requested run kinds")
     return dst[: out_len.value].copy(), offs
+
+
+# ---- byte / boolean RLE ------------------------------------------------------
+class ByteRleDecoder:
+    """Drop-in for orc::ByteRleDecoder (createByteRleDecoder /
+    createBooleanRleDecoder, c++/src/ByteRLE.hh:114,126): bulk GPU decode at
+    construction, then next(n, notNull) / skip(n) / seek(positions)."""
+
+    def __init__(self, data, boolean=False, ctx=None):
+        self._L = _lib.load()
+        self.ctx = ctx or default_context()
+        self.boolean = boolean
+        self._buf = np.frombuffer(bytes(data), dtype=np.uint8).copy()
+        h = ctypes.c_void_p()
+        check(self._L.orcg_byte_rle_decoder_create(self.ctx.handle, _ptr(self._buf), self._buf.size,
+                                                   int(bool(boolean)), ctypes.byref(h)), self.ctx.last_error)
+        self._h = h
+
+    def _err(self):
+        return self._L.orcg_byte_rle_decoder_last_error(self._h)
+
+    def next(self, n, not_null=None, out=None):
+        if out is None:
+            out = np.zeros(n, dtype=np.uint8)
+        nn = None if not_null is None else np.ascontiguousarray(not_null, dtype=np.uint8)
+        check(self._L.orcg_byte_rle_decoder_next(self._h, _ptr(out), n, _ptr(nn)), self._err)
+        return out
+
+    def skip(self, n):
+        check(self._L.orcg_byte_rle_decoder_skip(self._h, n), self._err)
+
+    def seek(self, *positions):
+        p = np.asarray(positions, dtype=np.uint64)
+        check(self._L.orcg_byte_rle_decoder_seek(self._h, _ptr(p), p.size), self._err)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.orcg_byte_rle_decoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def create_byte_rle_decoder(data, ctx=None):
+    return ByteRleDecoder(data, boolean=False, ctx=ctx)
+
+
+def create_boolean_rle_decoder(data, ctx=None):
+    return ByteRleDecoder(data, boolean=True, ctx=ctx)
+
+
+class BytePlan(Plan):
+    """orcg_byterle_plan_create: control-byte walk -> segments."""
+
+    def __init__(self, data, max_segment_bytes=16 << 10, max_segment_values=16384):
+        self._L = _lib.load()
+        self._buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        h = ctypes.c_void_p()
+        check(self._L.orcg_byterle_plan_create(_ptr(self._buf), self._buf.size, max_segment_bytes,
+                                               max_segment_values, ctypes.byref(h)))
+        self._h = h
+
+
+def byterle_decode_device(ctx, src, segments, nvalues, out, value_begin=0, boolean=False):
+    """Device-resident byte RLE (decoded bytes) or boolean RLE (one 0/1 char
+    per row) decode; torch tensors, asynchronous on the context stream."""
+    L = _lib.load()
+    fn = L.orcg_boolrle_decode_device if boolean else L.orcg_byterle_decode_device
+    check(fn(ctx.handle, _tensor_ptr(src), src.numel(), _tensor_ptr(segments), segments.shape[0], value_begin,
+             nvalues, _tensor_ptr(out)), ctx.last_error)
+    return out
+
+
+def scatter_not_null_device(ctx, dense, not_null, out, fill=None):
+    """dense values -> non-null rows of out (null slots untouched, or `fill`)."""
+    L = _lib.load()
+    check(L.orcg_scatter_not_null_device(ctx.handle, _tensor_ptr(dense), _tensor_ptr(not_null), not_null.numel(),
+                                         _tensor_ptr(out), out.element_size(), 0 if fill is None else 1,
+                                         0 if fill is None else int(fill)), ctx.last_error)
+    return out
+
+
+def dict_offsets_device(ctx, lengths, offsets):
+    L = _lib.load()
+    check(L.orcg_dict_offsets_device(ctx.handle, _tensor_ptr(lengths), lengths.numel(), _tensor_ptr(offsets)),
+          ctx.last_error)
+    return offsets
+
+
+def dict_gather_device(ctx, indices, offsets, start, length, not_null=None):
+    L = _lib.load()
+    nn = None if not_null is None else _tensor_ptr(not_null)
+    check(L.orcg_dict_gather_device(ctx.handle, _tensor_ptr(indices), indices.element_size(), nn, indices.numel(),
+                                    _tensor_ptr(offsets), offsets.numel() - 1, _tensor_ptr(start),
+                                    _tensor_ptr(length)), ctx.last_error)
+    return start, length
+
+
+def decode_integer_column(present, data, n, is_signed=True, ctx=None):
+    """IntegerColumnReader::next over a stripe column: (values, not_null);
+    null slots of `values` stay 0 (untouched)."""
+    L = _lib.load()
+    ctx = ctx or default_context()
+    pb = None if present is None else np.frombuffer(bytes(present), dtype=np.uint8)
+    db = np.frombuffer(bytes(data), dtype=np.uint8)
+    out = np.zeros(n, dtype=np.int64)
+    nn = np.zeros(n, dtype=np.uint8)
+    check(L.orcg_decode_integer_column(ctx.handle, _ptr(pb), 0 if pb is None else pb.size, _ptr(db), db.size,
+                                       int(bool(is_signed)), n, _ptr(out), _ptr(nn)), ctx.last_error)
+    return out, nn
