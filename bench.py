@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--variant", type=int, default=0, help="0 tiled (default), 1 wave-walk")
+    ap.add_argument("--copy-inclusive", type=int, default=3,
+                    help="steps of the PCIe-inclusive pipeline to time (host bytes -> host values); 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,6 +161,28 @@ def main():
         dist.barrier()
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
 
+    copy_incl = None
+    if args.copy_inclusive and rank == 0:
+        # host stream bytes (pinned) -> H2D -> decode -> D2H into a pinned
+        # host column: the rate a host-memory caller sees
+        h_src = torch.from_numpy(data).pin_memory()
+        h_out = torch.empty(N, dtype=torch.int64).pin_memory()
+        ts = []
+        for _ in range(args.copy_inclusive + 1):
+            torch.cuda.synchronize()
+            c0 = time.perf_counter()
+            with torch.cuda.stream(stream):
+                d_src.copy_(h_src, non_blocking=True)
+                step()
+                h_out.copy_(d_out, non_blocking=True)
+            stream.synchronize()
+            ts.append(time.perf_counter() - c0)
+        t_ci = float(np.median(ts[1:]))
+        copy_incl = {"GBps_decoded": round(8 * N / t_ci / 1e9, 2), "ms": round(t_ci * 1e3, 3),
+                     "h2d_bytes": S, "d2h_bytes": 8 * N}
+        if not args.no_verify and not torch.equal(h_out, torch.from_numpy(values)):
+            raise SystemExit("copy-inclusive decode mismatch")
+
     if rank == 0:
         rows_total = N * world
         ms_per_step = elapsed * 1e3 / args.steps
@@ -201,6 +225,8 @@ def main():
                 "algorithmic_bytes_per_launch": algo_bytes,
             },
         }
+        if copy_incl:
+            line["copy_inclusive"] = copy_incl
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(data, N, args.cpu_budget)
         print(json.dumps(line), flush=True)
