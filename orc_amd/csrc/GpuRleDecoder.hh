@@ -111,11 +111,13 @@ class ByteRleDecoder {
 };
 
 // GPU RLEv2 decoder: the stream is bulk-decoded on the device on creation.
+// (The status is read before the message: the message buffer is only valid
+// after the call that set it.)
 class GpuRleDecoderV2 : public RleDecoder {
  public:
   GpuRleDecoderV2(Context& ctx, const uint8_t* data, uint64_t len, bool isSigned) {
-    throwOnError(orcg_rle_decoder_create(ctx.get(), data, len, isSigned ? 1 : 0, 2, &dec_),
-                 orcg_ctx_last_error(ctx.get()));
+    const int rc = orcg_rle_decoder_create(ctx.get(), data, len, isSigned ? 1 : 0, 2, &dec_);
+    throwOnError(rc, orcg_ctx_last_error(ctx.get()));
   }
   ~GpuRleDecoderV2() override { orcg_rle_decoder_destroy(dec_); }
 
@@ -123,22 +125,16 @@ class GpuRleDecoderV2 : public RleDecoder {
   void seek(PositionProvider& location) override {
     std::vector<uint64_t> p = location.remaining();
     if (p.size() > 2) p.resize(2);
-    throwOnError(orcg_rle_decoder_seek(dec_, p.data(), p.size()), err());
+    check(orcg_rle_decoder_seek(dec_, p.data(), p.size()));
     location.consume(p.size());
   }
-  void skip(uint64_t n) override { throwOnError(orcg_rle_decoder_skip(dec_, n), err()); }
-  void next(int64_t* d, uint64_t n, const char* nn) override {
-    throwOnError(orcg_rle_decoder_next_i64(dec_, d, n, nn), err());
-  }
-  void next(int32_t* d, uint64_t n, const char* nn) override {
-    throwOnError(orcg_rle_decoder_next_i32(dec_, d, n, nn), err());
-  }
-  void next(int16_t* d, uint64_t n, const char* nn) override {
-    throwOnError(orcg_rle_decoder_next_i16(dec_, d, n, nn), err());
-  }
+  void skip(uint64_t n) override { check(orcg_rle_decoder_skip(dec_, n)); }
+  void next(int64_t* d, uint64_t n, const char* nn) override { check(orcg_rle_decoder_next_i64(dec_, d, n, nn)); }
+  void next(int32_t* d, uint64_t n, const char* nn) override { check(orcg_rle_decoder_next_i32(dec_, d, n, nn)); }
+  void next(int16_t* d, uint64_t n, const char* nn) override { check(orcg_rle_decoder_next_i16(dec_, d, n, nn)); }
 
  private:
-  const char* err() const { return orcg_rle_decoder_last_error(dec_); }
+  void check(int rc) const { throwOnError(rc, orcg_rle_decoder_last_error(dec_)); }
   orcg_rle_decoder* dec_ = nullptr;
 };
 
@@ -146,24 +142,22 @@ class GpuRleDecoderV2 : public RleDecoder {
 class GpuByteRleDecoder : public ByteRleDecoder {
  public:
   GpuByteRleDecoder(Context& ctx, const uint8_t* data, uint64_t len, bool boolean) : boolean_(boolean) {
-    throwOnError(orcg_byte_rle_decoder_create(ctx.get(), data, len, boolean ? 1 : 0, &dec_),
-                 orcg_ctx_last_error(ctx.get()));
+    const int rc = orcg_byte_rle_decoder_create(ctx.get(), data, len, boolean ? 1 : 0, &dec_);
+    throwOnError(rc, orcg_ctx_last_error(ctx.get()));
   }
   ~GpuByteRleDecoder() override { orcg_byte_rle_decoder_destroy(dec_); }
   void seek(PositionProvider& location) override {
     std::vector<uint64_t> p = location.remaining();
     const size_t k = boolean_ ? 3 : 2;
     if (p.size() > k) p.resize(k);
-    throwOnError(orcg_byte_rle_decoder_seek(dec_, p.data(), p.size()), err());
+    check(orcg_byte_rle_decoder_seek(dec_, p.data(), p.size()));
     location.consume(p.size());
   }
-  void skip(uint64_t n) override { throwOnError(orcg_byte_rle_decoder_skip(dec_, n), err()); }
-  void next(char* d, uint64_t n, char* nn) override {
-    throwOnError(orcg_byte_rle_decoder_next(dec_, d, n, nn), err());
-  }
+  void skip(uint64_t n) override { check(orcg_byte_rle_decoder_skip(dec_, n)); }
+  void next(char* d, uint64_t n, char* nn) override { check(orcg_byte_rle_decoder_next(dec_, d, n, nn)); }
 
  private:
-  const char* err() const { return orcg_byte_rle_decoder_last_error(dec_); }
+  void check(int rc) const { throwOnError(rc, orcg_byte_rle_decoder_last_error(dec_)); }
   orcg_byte_rle_decoder* dec_ = nullptr;
   bool boolean_;
 };

@@ -36,6 +36,7 @@ constexpr int kMaxRuns = 512;       // run-table capacity per window
 constexpr int kOptNTStore = 1;  // non-temporal output stores (streamed, never re-read)
 constexpr int kOptNTLoad = 2;   // non-temporal LDS-DMA loads of the stream
 constexpr int kOptReuse = 4;    // carry the window tail over in LDS; never load past the segment
+constexpr int kOptFast = 8;     // predicate-free path for full DIRECT runs inside the output range
 
 template <int kOpt, typename T>
 __device__ __forceinline__ void store1(T* p, uint64_t v) {
@@ -100,6 +101,35 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
   }
   if (r.kind == 1) {
     const uint32_t W = r.W;
+    if ((kOpt & kOptFast) && L == 512 && v0 >= value_begin && v0 + 512 <= value_end) {
+      // Full run entirely inside the output range: no per-value predicates.
+      T* out = dst + (v0 - value_begin);
+      if (W == 64) {
+        // 8 bytes per value at d + 8j: one uniform byte alignment per run
+        const uint32_t r4 = d & 3u;
+#pragma unroll
+        for (int it = 0; it < kMaxRunUnroll; ++it) {
+          const uint32_t j = it * kWave + lane;
+          const u32x3 w = lds12(win, d + 8 * j);
+          const uint32_t lo = __builtin_amdgcn_alignbyte(w.y, w.x, r4);
+          const uint32_t hi = __builtin_amdgcn_alignbyte(w.z, w.y, r4);
+          uint64_t v = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
+          if (is_signed) v = unzigzag(v);
+          store1<kOpt>(out + j, v);
+        }
+      } else {
+#pragma unroll
+        for (int it = 0; it < kMaxRunUnroll; ++it) {
+          const uint32_t j = it * kWave + lane;
+          const uint32_t bit = j * W;
+          const uint32_t br = d + (bit >> 3);
+          uint64_t v = field(lds12(win, br), br, bit & 7u, W);
+          if (is_signed) v = unzigzag(v);
+          store1<kOpt>(out + j, v);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int it = 0; it < kMaxRunUnroll; ++it) {
       if ((uint32_t)it < niter) {
@@ -115,21 +145,15 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
     return;
   }
   if (r.kind == 2) {
-    // Literals into registers, then the patch list walked in order exactly as
-    // nextPatched (:340-366) with adjustGapAndPatch (:250-271): an escape
-    // (gap 255, patch 0) only advances; a patch that does not move past the
-    // previous one stalls the walk; positions >= L are never reached.
+    // PATCHED_BASE. The patch list (<= 31 entries of cfb bits) is held one
+    // entry per lane; positions are the inclusive prefix sum of the gap
+    // fields (an escape entry, gap 255 / patch 0, contributes its 255), and
+    // the entries are applied in order exactly like nextPatched's loop
+    // (:340-366) with adjustGapAndPatch (:250-271): escapes only advance, a
+    // patch that does not move past the previous one stalls the walk, and
+    // positions >= L are never reached. Low register footprint: one 64-value
+    // chunk of literals at a time, patches consumed with a scalar cursor.
     const uint32_t W = r.W;
-    uint64_t lit[kMaxRunUnroll];
-#pragma unroll
-    for (int it = 0; it < kMaxRunUnroll; ++it) {
-      lit[it] = 0;
-      if ((uint32_t)it < niter) {
-        const uint32_t bit = (it * kWave + lane) * W;
-        const uint32_t br = d + (bit >> 3);
-        lit[it] = field(lds12(win, br), br, bit & 7u, W);
-      }
-    }
     const uint32_t p0 = d + (W * L + 7) / 8;  // patch list
     uint64_t entry = 0;
     if ((uint32_t)lane < r.pl) {
@@ -138,29 +162,48 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
       entry = field(lds12(win, br), br, bit & 7u, r.cfb);
     }
     const uint64_t pmask = (1ull << r.pbs) - 1;  // pbs <= 63 (checked by the walk)
-    const uint32_t e_lo = (uint32_t)entry, e_hi = (uint32_t)(entry >> 32);
-    uint64_t cum = 0, prev = 0;
-    bool first = true;
-    for (uint32_t k = 0; k < r.pl; ++k) {
-      const uint64_t e = ((uint64_t)rdlane(e_hi, k) << 32) | rdlane(e_lo, k);
-      const uint64_t gp = e >> r.pbs, pv = e & pmask;
-      cum += gp;
-      if (gp == 255 && pv == 0) continue;
-      if ((!first && cum == prev) || cum >= L) break;
-      const uint32_t slot = (uint32_t)cum / kWave, who = (uint32_t)cum % kWave;
-      const uint64_t add = pv << (W & 63u);
+    const uint32_t gap = (uint32_t)lane < r.pl ? (uint32_t)(entry >> r.pbs) : 0u;  // <= 255
+    uint32_t cum = gap;  // wave inclusive scan (positions <= 31 * 255)
 #pragma unroll
-      for (int it = 0; it < kMaxRunUnroll; ++it)
-        if ((uint32_t)it == slot && (uint32_t)lane == who) lit[it] |= add;
-      prev = cum;
-      first = false;
+    for (int dd = 1; dd < kWave; dd <<= 1) {
+      const uint32_t y = __shfl_up(cum, dd, kWave);
+      if (lane >= dd) cum += y;
     }
-#pragma unroll
-    for (int it = 0; it < kMaxRunUnroll; ++it) {
+    const uint64_t patch = entry & pmask;
+    const uint32_t p_lo = (uint32_t)patch, p_hi = (uint32_t)(patch >> 32);
+    // scalar pass: which entries apply (bitmask over entries)
+    uint64_t applied = 0;
+    {
+      uint32_t prev = 0;
+      bool first = true;
+      for (uint32_t k = 0; k < r.pl; ++k) {
+        const uint32_t c = rdlane(cum, k), g = rdlane(gap, k);
+        const bool esc = g == 255 && rdlane(p_lo, k) == 0 && rdlane(p_hi, k) == 0;
+        if (esc) continue;
+        if ((!first && c == prev) || c >= L) break;
+        applied |= 1ull << k;
+        prev = c;
+        first = false;
+      }
+    }
+    uint64_t todo = applied;
+#pragma unroll 1
+    for (uint32_t it = 0; it < niter; ++it) {
       const uint32_t j = it * kWave + lane;
+      const uint32_t bit = j * W;
+      const uint32_t br = d + (bit >> 3);
+      uint64_t lit = field(lds12(win, br), br, bit & 7u, W);
+      // patches whose position falls in this chunk (positions increase)
+      while (todo) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(todo);
+        const uint32_t c = rdlane(cum, k);
+        if (c / kWave != it) break;
+        const uint64_t pv = ((uint64_t)rdlane(p_hi, k) << 32) | rdlane(p_lo, k);
+        if ((uint32_t)lane == c % kWave) lit |= pv << (W & 63u);
+        todo &= todo - 1;
+      }
       const uint64_t o = v0 + j;
-      if ((uint32_t)it < niter && j < L && o >= value_begin && o < value_end)
-        store1<kOpt>(dst + (o - value_begin), r.a + lit[it]);
+      if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), r.a + lit);
     }
     return;
   }
@@ -179,23 +222,21 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
   const uint64_t v1 = r.a + r.b;
   const bool neg = (int64_t)r.b < 0;
   uint64_t carry = 0;
-#pragma unroll
-  for (int it = 0; it < kMaxRunUnroll; ++it) {
-    if ((uint32_t)it < niter) {
-      const uint32_t j = it * kWave + lane;
-      const int32_t k = (int32_t)j - 2;
-      uint64_t dlt = 0;
-      if (k >= 0 && j < L) {
-        const uint32_t bit = (uint32_t)k * W;
-        const uint32_t br = d + (bit >> 3);
-        dlt = field(lds12(win, br), br, bit & 7u, W);
-      }
-      const uint64_t sum = wave_inclusive_scan(dlt, lane) + carry;
-      carry = (uint64_t)__shfl(sum, kWave - 1, kWave);
-      const uint64_t v = j == 0 ? r.a : (j == 1 ? v1 : (neg ? v1 - sum : v1 + sum));
-      const uint64_t o = v0 + j;
-      if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), v);
+#pragma unroll 1
+  for (uint32_t it = 0; it < niter; ++it) {
+    const uint32_t j = it * kWave + lane;
+    const int32_t k = (int32_t)j - 2;
+    uint64_t dlt = 0;
+    if (k >= 0 && j < L) {
+      const uint32_t bit = (uint32_t)k * W;
+      const uint32_t br = d + (bit >> 3);
+      dlt = field(lds12(win, br), br, bit & 7u, W);
     }
+    const uint64_t sum = wave_inclusive_scan(dlt, lane) + carry;
+    carry = (uint64_t)__shfl(sum, kWave - 1, kWave);
+    const uint64_t v = j == 0 ? r.a : (j == 1 ? v1 : (neg ? v1 - sum : v1 + sum));
+    const uint64_t o = v0 + j;
+    if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), v);
   }
 }
 
@@ -435,15 +476,25 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
   } while (0)
 
   switch (ctx->rlev2_variant) {
-    case 2: ORCG_KT(kOptNTStore, 33, false, 1); break;                // no tail reuse
-    case 3: ORCG_KT(kOptReuse, 33, false, 1); break;                  // plain stores
-    case 4: ORCG_KT(kOptNTStore, 17, true, 1); break;                 // pipelined 2 x 17 KB
-    case 5: ORCG_KT(kOptNTStore | kOptReuse, 17, false, 1); break;    // 17 KB window
-    case 6: ORCG_KT(kOptNTStore | kOptReuse, 25, false, 5); break;    // 25 KB, <= 96 VGPR
-    case 7: ORCG_KT(kOptNTStore | kOptReuse, 17, false, 6); break;    // 17 KB, <= 80 VGPR
-    case 8: ORCG_KT(kOptNTStore | kOptReuse, 17, false, 8); break;    // 17 KB, <= 64 VGPR
-    case 9: ORCG_KT(kOptNTStore | kOptReuse, 12, false, 8); break;    // 12 KB, <= 64 VGPR
-    default: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1); break;   // 0: 33 KB, reuse, nt stores
+    case 2: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 33, false, 1); break;  // + full-run fast path
+    case 3: ORCG_KT(kOptReuse, 33, false, 1); break;                           // plain stores
+    case 4: ORCG_KT(kOptNTStore, 17, true, 1); break;                          // pipelined 2 x 17 KB
+    case 5: ORCG_KT(kOptNTStore | kOptReuse, 17, false, 6); break;             // 17 KB, 6 WG/CU
+    case 6: ORCG_KT(kOptNTStore | kOptReuse, 25, false, 5); break;             // 25 KB, 5 WG/CU
+    case 7: ORCG_KT(kOptNTStore | kOptReuse, 21, false, 6); break;             // 21 KB, 6 WG/CU
+    case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6); break;  // 21 KB + fast
+    case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1); break;             // 33 KB, 4 WG/CU
+    default: {
+      // ORCG_RLEV2_TILED picks the window by stream density: wide values
+      // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
+      // 33 KB windows (4 WG/CU); narrower ones need more workgroups in
+      // flight per CU to keep HBM busy: 21 KB windows (6 WG/CU) + the
+      // predicate-free full-run path. Measured: scripts/ab_rlev2.py.
+      const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
+      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1);
+      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6);
+      break;
+    }
   }
 #undef ORCG_KT
 #undef ORCG_K

@@ -24,8 +24,8 @@ for s in $STEPS; do
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py ;;
     drift) run drift 300 python scripts/drift.py ;;
-    ab) run ab 600 python scripts/ab_rlev2.py --variants 0,2,5 ;;
-    ab13) run ab13 600 python scripts/ab_rlev2.py --bits 13 --variants 0,2,5 ;;
+    ab) run ab 600 python scripts/ab_rlev2.py --variants 0,1,8,9 ;;
+    ab13) run ab13 600 python scripts/ab_rlev2.py --bits 13 --variants 0,1,8,9 ;;
     benchwalk) run bench_walk 600 python bench.py --variant 1 --no-cpu-baseline ;;
     prof)
       export TMPDIR=/tmp

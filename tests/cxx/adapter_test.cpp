@@ -73,9 +73,16 @@ int main(int argc, char** argv) {
     int64_t v[10];
     try {
       rle->next(v, 10, nullptr);
+      std::cerr << "no ParseError for pl==0\n";
       ++failures;
     } catch (const ParseError& e) {
-      if (std::string(e.what()) != "Corrupt PATCHED_BASE encoded data (pl==0)!") ++failures;
+      if (std::string(e.what()) != "Corrupt PATCHED_BASE encoded data (pl==0)!") {
+        std::cerr << "pl==0 message: " << e.what() << "\n";
+        ++failures;
+      }
+    } catch (const std::exception& e) {
+      std::cerr << "pl==0 wrong exception type: " << e.what() << "\n";
+      ++failures;
     }
   }
   // seek through a PositionProvider (c++/test/TestRleDecoder.cc:717-744)
@@ -87,7 +94,10 @@ int main(int argc, char** argv) {
     rle->seek(loc);
     int64_t d[3];
     rle->next(d, 3, nullptr);
-    if (d[0] != 2 || d[1] != 0 || d[2] != 2) ++failures;
+    if (d[0] != 2 || d[1] != 0 || d[2] != 2) {
+      std::cerr << "seek: " << d[0] << " " << d[1] << " " << d[2] << "\n";
+      ++failures;
+    }
   }
   std::printf("%s %d cases, %d failures\n", failures ? "FAIL" : "OK", cases, failures);
   return failures ? 1 : 0;
