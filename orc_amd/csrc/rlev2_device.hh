@@ -51,14 +51,45 @@ __device__ __forceinline__ uint64_t field(u32x3 w, uint32_t rel, uint32_t sh, ui
   return (be << sh) >> (64 - W);
 }
 
-// Wavefront inclusive prefix sum of a 64-bit value.
-__device__ __forceinline__ uint64_t wave_inclusive_scan(uint64_t x, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint64_t y = __shfl_up(x, d, kWave);
-    if (lane >= d) x += y;
-  }
+// Wavefront inclusive prefix sums on DPP (no LDS round trips): Kogge-Stone
+// inside each 16-lane row with row_shr:1,2,4,8, then row_bcast:15 (rows 1,3)
+// and row_bcast:31 (rows 2,3) carry the row totals across. Requires all 64
+// lanes active. Invalid source lanes read 0 (bound_ctrl).
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kCtrl, kRowMask, 0xf, true);
+}
+
+__device__ __forceinline__ uint32_t wave_scan_u32(uint32_t x) {
+  x += dpp0<0x111, 0xf>(x);  // row_shr:1
+  x += dpp0<0x112, 0xf>(x);  // row_shr:2
+  x += dpp0<0x114, 0xf>(x);  // row_shr:4
+  x += dpp0<0x118, 0xf>(x);  // row_shr:8
+  x += dpp0<0x142, 0xa>(x);  // row_bcast:15
+  x += dpp0<0x143, 0xc>(x);  // row_bcast:31
   return x;
+}
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint64_t dpp0_64(uint64_t x) {
+  const uint32_t lo = dpp0<kCtrl, kRowMask>((uint32_t)x), hi = dpp0<kCtrl, kRowMask>((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_inclusive_scan(uint64_t x, int /*lane*/ = 0) {
+  x += dpp0_64<0x111, 0xf>(x);
+  x += dpp0_64<0x112, 0xf>(x);
+  x += dpp0_64<0x114, 0xf>(x);
+  x += dpp0_64<0x118, 0xf>(x);
+  x += dpp0_64<0x142, 0xa>(x);
+  x += dpp0_64<0x143, 0xc>(x);
+  return x;
+}
+
+// Value of lane 63 (wave-uniform, scalar register).
+__device__ __forceinline__ uint64_t last_lane(uint64_t x) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), 63) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, 63);
 }
 
 __device__ __forceinline__ void report(unsigned long long* err, uint64_t value_index, uint32_t code) {

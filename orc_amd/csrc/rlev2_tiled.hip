@@ -163,12 +163,7 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
     }
     const uint64_t pmask = (1ull << r.pbs) - 1;  // pbs <= 63 (checked by the walk)
     const uint32_t gap = (uint32_t)lane < r.pl ? (uint32_t)(entry >> r.pbs) : 0u;  // <= 255
-    uint32_t cum = gap;  // wave inclusive scan (positions <= 31 * 255)
-#pragma unroll
-    for (int dd = 1; dd < kWave; dd <<= 1) {
-      const uint32_t y = __shfl_up(cum, dd, kWave);
-      if (lane >= dd) cum += y;
-    }
+    const uint32_t cum = wave_scan_u32(gap);  // positions (<= 31 * 255)
     const uint64_t patch = entry & pmask;
     const uint32_t p_lo = (uint32_t)patch, p_hi = (uint32_t)(patch >> 32);
     // scalar pass: which entries apply (bitmask over entries)
@@ -221,7 +216,28 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
   const uint32_t W = r.W;
   const uint64_t v1 = r.a + r.b;
   const bool neg = (int64_t)r.b < 0;
-  uint64_t carry = 0;
+  uint64_t carry = 0;  // wave-uniform running |delta| total
+  if (W <= 26) {
+    // 64 deltas of <= 26 bits sum below 2^32: scan in 32 bits
+#pragma unroll 1
+    for (uint32_t it = 0; it < niter; ++it) {
+      const uint32_t j = it * kWave + lane;
+      const int32_t k = (int32_t)j - 2;
+      uint32_t dlt = 0;
+      if (k >= 0 && j < L) {
+        const uint32_t bit = (uint32_t)k * W;
+        const uint32_t br = d + (bit >> 3);
+        dlt = (uint32_t)field(lds12(win, br), br, bit & 7u, W);
+      }
+      const uint32_t s32 = wave_scan_u32(dlt);
+      const uint64_t sum = carry + s32;
+      carry += (uint32_t)__builtin_amdgcn_readlane((int)s32, 63);
+      const uint64_t v = j == 0 ? r.a : (j == 1 ? v1 : (neg ? v1 - sum : v1 + sum));
+      const uint64_t o = v0 + j;
+      if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), v);
+    }
+    return;
+  }
 #pragma unroll 1
   for (uint32_t it = 0; it < niter; ++it) {
     const uint32_t j = it * kWave + lane;
@@ -232,8 +248,8 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
       const uint32_t br = d + (bit >> 3);
       dlt = field(lds12(win, br), br, bit & 7u, W);
     }
-    const uint64_t sum = wave_inclusive_scan(dlt, lane) + carry;
-    carry = (uint64_t)__shfl(sum, kWave - 1, kWave);
+    const uint64_t sum = wave_inclusive_scan(dlt) + carry;
+    carry = last_lane(sum);
     const uint64_t v = j == 0 ? r.a : (j == 1 ? v1 : (neg ? v1 - sum : v1 + sum));
     const uint64_t o = v0 + j;
     if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), v);
@@ -350,9 +366,12 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         const uint64_t end_rel = (seg_end - bias + 15) & ~15ull;
         if (end_rel - wrel < need) need = (uint32_t)(end_rel - wrel);
         // the previous window's tail [wpos, pwpos + pneed) is already in LDS:
-        // move it to the front instead of re-reading it (disjoint ranges,
-        // since wpos - pwpos >= kWin - kMaxRun - 16 > kMaxRun + 16 >= keep)
-        if (pwpos != ~0ull && pwpos + pneed > wpos) {
+        // move it to the front instead of re-reading it (source and
+        // destination must not overlap: the shift is at least the length)
+        // A walk that stopped on a full run table (many tiny runs) may have
+        // advanced less than the tail it would keep: then reload instead of
+        // an overlapping LDS move.
+        if (pwpos != ~0ull && pwpos + pneed > wpos && wpos - pwpos >= pwpos + pneed - wpos) {
           keep = (uint32_t)(pwpos + pneed - wpos);
           if (keep > need) keep = need;
           const uint32_t so = (uint32_t)(wpos - pwpos);
@@ -476,12 +495,6 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
   } while (0)
 
   switch (ctx->rlev2_variant) {
-    case 2: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 33, false, 1); break;  // + full-run fast path
-    case 3: ORCG_KT(kOptReuse, 33, false, 1); break;                           // plain stores
-    case 4: ORCG_KT(kOptNTStore, 17, true, 1); break;                          // pipelined 2 x 17 KB
-    case 5: ORCG_KT(kOptNTStore | kOptReuse, 17, false, 6); break;             // 17 KB, 6 WG/CU
-    case 6: ORCG_KT(kOptNTStore | kOptReuse, 25, false, 5); break;             // 25 KB, 5 WG/CU
-    case 7: ORCG_KT(kOptNTStore | kOptReuse, 21, false, 6); break;             // 21 KB, 6 WG/CU
     case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6); break;  // 21 KB + fast
     case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1); break;             // 33 KB, 4 WG/CU
     default: {

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--stride", type=int, default=10_000)
+    ap.add_argument("--data", default="random", choices=["random", "delta", "repeat", "patched"])
     args = ap.parse_args()
     import torch
 
@@ -27,11 +28,45 @@ def main():
 
     rng = np.random.default_rng(42)
     n = args.rows
-    if args.bits == 64:
-        v = rng.integers(-(1 << 63), (1 << 63) - 1, size=n, dtype=np.int64, endpoint=True)
+    if args.data == "random":
+        if args.bits == 64:
+            v = rng.integers(-(1 << 63), (1 << 63) - 1, size=n, dtype=np.int64, endpoint=True)
+        else:
+            v = rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=n, dtype=np.int64)
+        data, pos = orc_amd.encode_direct(v, True, aligned=True, rows_per_group=args.stride)
     else:
-        v = rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=n, dtype=np.int64)
-    data, pos = orc_amd.encode_direct(v, True, aligned=True, rows_per_group=args.stride)
+        # structured columns through the run builder: sorted keys (DELTA
+        # runs of 512), low-cardinality repeats (SHORT_REPEAT runs of 3-10),
+        # small values with outliers (PATCHED_BASE runs of 512)
+        if args.data == "delta":
+            lens = np.full(n // 512, 512, dtype=np.uint32)
+            kinds = np.full(lens.size, 3, dtype=np.uint8)
+            v = np.cumsum(rng.integers(0, 1 << args.bits, size=n, dtype=np.int64)) + 1_000_000
+        elif args.data == "repeat":
+            lens = rng.integers(3, 11, size=n // 6 + 16).astype(np.uint32)
+            lens = lens[: np.searchsorted(np.cumsum(lens), n) + 1]
+            lens[-1] -= np.cumsum(lens)[-1] - n
+            if lens[-1] < 3:
+                lens = lens[:-1]
+                n = int(lens.sum())
+            kinds = np.zeros(lens.size, dtype=np.uint8)
+            v = np.repeat(rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=lens.size), lens)
+        else:
+            lens = np.full(n // 512, 512, dtype=np.uint32)
+            kinds = np.full(lens.size, 2, dtype=np.uint8)
+            v = rng.integers(0, 1 << args.bits, size=n, dtype=np.int64)
+            out = rng.random(n) < 0.004
+            v[out] += rng.integers(1 << 40, 1 << 44, size=int(out.sum()))
+            v[::512] = 0  # keep a small base per run
+            v[100::512] += 1 << 41  # and at least one patch (pl == 0 is corrupt)
+        n = int(lens.sum())
+        v = v[:n].astype(np.int64)
+        data, offs = orc_amd.encode_runs(v, True, kinds, lens)
+        # positions: first run of every row group (stride-aligned run starts)
+        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        g = np.arange(0, n, args.stride)
+        ri = np.searchsorted(starts, g, side="right") - 1
+        pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
     S = data.size
     stream = torch.cuda.Stream()
     ctx = orc_amd.Context(0, stream=stream)
@@ -57,12 +92,22 @@ def main():
             ctx.set_rlev2_variant(var)
             orc_amd.decode_positions_device(ctx, d_src, d_pos, args.stride, n, True, d_out)
 
-    # verify every variant once
+    # verify every variant once; a mismatching variant is reported and dropped
+    bad = []
     for var in variants:
-        d_out.zero_()
+        with torch.cuda.stream(stream):  # same stream as the decode (torch streams do not sync)
+            d_out.zero_()
         run(var)
         ctx.synchronize()
-        assert torch.equal(d_out, d_vals), "variant %d mismatch" % var
+        if not torch.equal(d_out, d_vals):
+            idx = torch.nonzero(d_out != d_vals).flatten()
+            i0 = int(idx[0])
+            print(json.dumps({"variant": var, "mismatch": int(idx.numel()), "first": i0,
+                              "group": i0 // args.stride, "in_group": i0 % args.stride,
+                              "expected": d_vals[i0:i0 + 4].tolist(), "got": d_out[i0:i0 + 4].tolist(),
+                              "last": int(idx[-1])}), flush=True)
+            bad.append(var)
+    variants = [v for v in variants if v not in bad]
     refs = ["copy", "probe0", "probe1", "probe2", "probe3"]
     times = {var: [] for var in refs + variants}
     for _ in range(args.rounds):
@@ -80,9 +125,11 @@ def main():
     for var, ts in times.items():
         ms = float(np.median(ts))
         byts = 16 * n if isinstance(var, str) else S + 8 * n
-        print(json.dumps({"variant": var, "bits": args.bits, "ms_median": round(ms, 4),
+        print(json.dumps({"variant": var, "bits": args.bits, "data": args.data, "stream_B_per_value": round(S / n, 3), "ms_median": round(ms, 4),
                           "ms_min": round(float(np.min(ts)), 4),
                           "GBps": round(byts / ms / 1e6, 1), "bytes": int(byts)}), flush=True)
+    if bad:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

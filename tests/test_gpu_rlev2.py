@@ -191,3 +191,68 @@ def test_large_roundtrip_property(orc):
                                 10_000, n, True, out)
     ctx.synchronize()
     assert torch.equal(out, v)
+
+
+def _stream_with_positions(orc, rng, kind, n, stride, bits=12):
+    if kind == "repeat":
+        lens = rng.integers(3, 11, size=n // 3).astype(np.uint32)
+        lens = lens[: np.searchsorted(np.cumsum(lens), n)]
+        kinds = np.zeros(lens.size, dtype=np.uint8)
+        v = np.repeat(rng.integers(-(1 << (bits - 1)), 1 << (bits - 1), size=lens.size), lens)
+    elif kind == "delta":
+        lens = np.full(n // 512, 512, dtype=np.uint32)
+        lens[::7] = 300  # ragged runs too
+        kinds = np.full(lens.size, 3, dtype=np.uint8)
+        v = np.cumsum(rng.integers(0, 1 << bits, size=int(lens.sum()), dtype=np.int64))
+        sgn = np.repeat(np.where(np.arange(lens.size) % 2 == 0, 1, -1), lens)
+        v = v * sgn  # alternate increasing / decreasing runs
+        # each run must be monotone in its own direction: rebuild per run
+        out, at = [], 0
+        for L, s in zip(lens, np.where(np.arange(lens.size) % 2 == 0, 1, -1)):
+            base = int(rng.integers(-(1 << 40), 1 << 40))
+            out.append(base + s * np.cumsum(rng.integers(1, 1 << bits, size=int(L))))
+        v = np.concatenate(out)
+    else:  # patched
+        lens = np.full(n // 512, 512, dtype=np.uint32)
+        kinds = np.full(lens.size, 2, dtype=np.uint8)
+        v = rng.integers(0, 1 << bits, size=int(lens.sum()), dtype=np.int64)
+        hot = rng.random(v.size) < 0.01
+        v[hot] += rng.integers(1 << 30, 1 << 50, size=int(hot.sum()))
+        v[100::512] += 1 << 33
+        v[::512] = 0
+    n = int(lens.sum())
+    v = v[:n].astype(np.int64)
+    data, offs = orc.encode_runs(v, True, kinds, lens)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    g = np.arange(0, n, stride)
+    ri = np.searchsorted(starts, g, side="right") - 1
+    pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
+    return v, data, pos
+
+
+@pytest.mark.parametrize("kind", ["repeat", "delta", "patched"])
+def test_structured_streams_every_variant(kind):
+    """Every kernel variant (ORCG_RLEV2_* and the tuning variants) is
+    bit-exact on SR-heavy (run tables that fill up), DELTA-heavy and
+    PATCHED-heavy streams, with one huge segment and with row groups."""
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng({"repeat": 1, "delta": 2, "patched": 3}[kind])
+    ctx = orc_amd.default_context(0)
+    for stride in (10_000, 1 << 30):
+        v, data, pos = _stream_with_positions(orc_amd, rng, kind, 300_000, stride)
+        want = oracle.rlev2_decode(data.tobytes(), v.size, True)
+        np.testing.assert_array_equal(want, v)
+        d_src = torch.from_numpy(data).cuda()
+        d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+        for variant in range(10):
+            ctx.set_rlev2_variant(variant)
+            out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, True, out)
+            ctx.synchronize()
+            got = out.cpu().numpy()
+            assert np.array_equal(got, want), "variant %d stride %d: first mismatch at %d" % (
+                variant, stride, int(np.argmax(got != want)))
+    ctx.set_rlev2_variant(0)
