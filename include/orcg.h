@@ -192,6 +192,22 @@ int orcg_byte_rle_decoder_skip(orcg_byte_rle_decoder* dec, uint64_t n);
 int orcg_byte_rle_decoder_seek(orcg_byte_rle_decoder* dec, const uint64_t* positions, uint64_t npositions);
 const char* orcg_byte_rle_decoder_last_error(const orcg_byte_rle_decoder* dec);
 
+/* ---- RLEv1 (DIRECT / DICTIONARY encodings, format 0.11 files) ------------
+ * Replaces RleDecoderV1 (c++/src/RLEv1.hh:51-96, RLEv1.cc:140-300) as chosen
+ * by createRleDecoder for RleVersion_1 (c++/src/RLE.cc:48-60). Plans cut the
+ * stream at control bytes; the plan accessors (orcg_rlev2_plan_*) apply.
+ * Truncated streams raise "bad read in readByte" (RLEv1.cc:141-146). */
+int orcg_rlev1_plan_create(const uint8_t* src, uint64_t src_len, uint64_t max_segment_bytes,
+                           uint64_t max_segment_values, orcg_rlev2_plan** out);
+int orcg_rlev1_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                             const orcg_segment* d_segs, uint64_t nsegs, uint64_t value_begin,
+                             uint64_t nvalues, void* d_dst, int dst_bytes);
+/* RleDecoderV1::next<T>(data, n, notNull) over a whole host stream. */
+int orcg_rlev1_decode_i64(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int is_signed,
+                          const char* not_null, uint64_t n, int64_t* data);
+int orcg_rlev1_decode_i32(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int is_signed,
+                          const char* not_null, uint64_t n, int32_t* data);
+
 /* ---- nullable columns and string dictionaries ----------------------------
  * Null scatter (RleDecoderV2::copyDataFromBuffer with notNull,
  * RleDecoderV2.cc:437-453): dense values -> the non-null rows of d_out

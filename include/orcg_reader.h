@@ -1,0 +1,125 @@
+/*
+ * orcg_reader.h — file-level C ABI of liborcgpu: ORC file bytes -> decoded
+ * column batches in HBM (and, on request, in host memory).
+ *
+ * Mirrors the reference's reader surface for the decode path:
+ *   orc::createReader / ReaderImpl            c++/include/orc/OrcFile.hh, c++/src/Reader.cc:1517-1700
+ *   Reader::getNumberOfRows/Stripes, getType  c++/include/orc/Reader.hh:460,529,620
+ *   RowReader::next(ColumnVectorBatch&)       c++/include/orc/Reader.hh:764 (one stripe per call here)
+ *   ColumnVectorBatch family                  c++/include/orc/Vector.hh:46-330
+ *   column readers (PRESENT / DATA / LENGTH / DICTIONARY_DATA per type)
+ *                                             c++/src/ColumnReader.cc:81-1160
+ *
+ * The host parses the tail and stripe footers and decompresses streams
+ * (zlib / snappy / lz4 / zstd stay on the CPU, as in the reference, which
+ * links those libraries); one H2D copy per stripe moves the stream bytes to
+ * HBM, where every integer, boolean, byte, length and dictionary stream is
+ * decoded by the HIP kernels of orcg.h. Batch layout per column (type id):
+ *   not_null : char[n], 1 = value present (NULL when the column has no nulls)
+ *   BOOLEAN, BYTE, SHORT, INT, LONG, DATE : int64 data[n]  (LongVectorBatch)
+ *   FLOAT, DOUBLE                         : double data[n] (DoubleVectorBatch)
+ *   STRING, VARCHAR, CHAR, BINARY         : int64 start[n] (blob-relative), int64 length[n],
+ *                                           blob = DATA (direct) or DICTIONARY_DATA bytes
+ *   LIST, MAP                             : int64 offsets[n + 1] (ListVectorBatch::offsets);
+ *                                           children hold offsets[n] rows
+ *   STRUCT                                : not_null only; children hold n rows
+ * Null slots hold 0 (the reference leaves them unspecified). TIMESTAMP,
+ * DECIMAL, UNION and TIMESTAMP_INSTANT columns are not decoded by this round
+ * (orcg_reader_column returns ORCG_INVALID_ARGUMENT for them).
+ */
+#ifndef ORCG_READER_H
+#define ORCG_READER_H
+
+#include "orcg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Type.Kind (ORCv1.md "Type Information") */
+enum {
+  ORCG_TYPE_BOOLEAN = 0, ORCG_TYPE_BYTE = 1, ORCG_TYPE_SHORT = 2, ORCG_TYPE_INT = 3, ORCG_TYPE_LONG = 4,
+  ORCG_TYPE_FLOAT = 5, ORCG_TYPE_DOUBLE = 6, ORCG_TYPE_STRING = 7, ORCG_TYPE_BINARY = 8,
+  ORCG_TYPE_TIMESTAMP = 9, ORCG_TYPE_LIST = 10, ORCG_TYPE_MAP = 11, ORCG_TYPE_STRUCT = 12,
+  ORCG_TYPE_UNION = 13, ORCG_TYPE_DECIMAL = 14, ORCG_TYPE_DATE = 15, ORCG_TYPE_VARCHAR = 16,
+  ORCG_TYPE_CHAR = 17, ORCG_TYPE_TIMESTAMP_INSTANT = 18
+};
+/* CompressionKind */
+enum { ORCG_COMPRESSION_NONE = 0, ORCG_COMPRESSION_ZLIB = 1, ORCG_COMPRESSION_SNAPPY = 2,
+       ORCG_COMPRESSION_LZO = 3, ORCG_COMPRESSION_LZ4 = 4, ORCG_COMPRESSION_ZSTD = 5 };
+
+typedef struct orcg_reader orcg_reader;
+
+typedef struct {
+  uint32_t kind;
+  uint32_t num_subtypes;
+  uint32_t maximum_length;
+  uint32_t precision;
+  uint32_t scale;
+} orcg_type_info;
+
+typedef struct {
+  uint64_t offset, index_length, data_length, footer_length, num_rows;
+} orcg_stripe_info;
+
+typedef struct {
+  uint32_t type_id;
+  uint32_t kind;          /* ORCG_TYPE_* */
+  uint32_t encoding;      /* ColumnEncoding.Kind of this stripe (DIRECT=0 .. DICTIONARY_V2=3) */
+  uint32_t decoded;       /* 1 if the column was decoded */
+  uint64_t num_elements;
+  int has_nulls;
+  const uint8_t* not_null; /* device */
+  const void* data;        /* device: int64 / double / int64 starts */
+  const int64_t* length;   /* device: string lengths */
+  const int64_t* offsets;  /* device: list / map offsets (n + 1) */
+  const uint8_t* blob;     /* device: string bytes */
+  uint64_t blob_len;
+} orcg_column_view;
+
+/* Open an ORC file held in host memory (the caller keeps `file` alive until
+ * orcg_reader_destroy) or on disk (memory-mapped). Parses PostScript and
+ * Footer; raises the reference's ParseError texts ("File size too small",
+ * "Invalid ORC postscript length", "Not an ORC file", ...). `ctx` may be
+ * NULL for metadata-only use (no GPU needed until a stripe is read). */
+int orcg_reader_open(orcg_ctx* ctx, const uint8_t* file, uint64_t file_len, orcg_reader** out);
+int orcg_reader_open_file(orcg_ctx* ctx, const char* path, orcg_reader** out);
+/* Message of this thread's last failed open (also in ctx's last error). */
+const char* orcg_reader_open_error(void);
+void orcg_reader_destroy(orcg_reader* r);
+const char* orcg_reader_last_error(const orcg_reader* r);
+
+uint64_t orcg_reader_num_rows(const orcg_reader* r);
+uint64_t orcg_reader_num_stripes(const orcg_reader* r);
+uint32_t orcg_reader_row_index_stride(const orcg_reader* r);
+uint32_t orcg_reader_compression(const orcg_reader* r);
+uint64_t orcg_reader_compression_block_size(const orcg_reader* r);
+/* file version [major, minor] (PostScript.version) */
+int orcg_reader_format_version(const orcg_reader* r, uint32_t* major, uint32_t* minor);
+uint32_t orcg_reader_writer_version(const orcg_reader* r);
+uint32_t orcg_reader_num_types(const orcg_reader* r);
+int orcg_reader_type(const orcg_reader* r, uint32_t type_id, orcg_type_info* out);
+int orcg_reader_subtypes(const orcg_reader* r, uint32_t type_id, uint32_t* out, uint32_t cap);
+const char* orcg_reader_field_name(const orcg_reader* r, uint32_t type_id, uint32_t i);
+int orcg_reader_stripe(const orcg_reader* r, uint64_t stripe, orcg_stripe_info* out);
+
+/* Column selection by type id (RowReaderOptions::include; NULL = all). A
+ * selected column's ancestors are read too. */
+int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes);
+
+/* Decode one stripe of the selected columns into device batches owned by the
+ * reader (valid until the next read or destroy). Synchronous. */
+int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe);
+int orcg_reader_column(const orcg_reader* r, uint32_t type_id, orcg_column_view* out);
+
+/* Device -> host copy on the reader's context stream (synchronous). */
+int orcg_reader_copy_to_host(orcg_reader* r, void* host_dst, const void* device_src, uint64_t bytes);
+
+/* Host time split of the last orcg_reader_read_stripe, in seconds:
+ * [0] tail/footer + chunk split, [1] decompression, [2] H2D, [3] decode (device). */
+int orcg_reader_last_timings(const orcg_reader* r, double* out4);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORCG_READER_H */

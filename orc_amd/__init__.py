@@ -26,8 +26,11 @@ from .rle import (  # noqa: F401
     default_context,
     encode_direct,
     encode_runs,
+    rlev1_decode,
     rlev2_decode,
     scatter_not_null_device,
 )
+
+from .reader import Reader, open_reader  # noqa: F401,E402
 
 __version__ = "0.1.0"

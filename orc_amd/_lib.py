@@ -72,6 +72,10 @@ SIGNATURES = [
     ("orcg_rle_decoder_seek", [vp, vp, u64], i32),
     ("orcg_rle_decoder_next_vector_java", [vp, vp, vp, u64, ctypes.POINTER(i32)], i32),
     ("orcg_rle_decoder_last_error", [vp], cp),
+    ("orcg_rlev1_plan_create", [vp, u64, u64, u64, ctypes.POINTER(vp)], i32),
+    ("orcg_rlev1_decode_device", [vp, vp, u64, i32, vp, u64, u64, u64, vp, i32], i32),
+    ("orcg_rlev1_decode_i64", [vp, vp, u64, i32, vp, u64, vp], i32),
+    ("orcg_rlev1_decode_i32", [vp, vp, u64, i32, vp, u64, vp], i32),
     ("orcg_byterle_plan_create", [vp, u64, u64, u64, ctypes.POINTER(vp)], i32),
     ("orcg_byterle_decode_device", [vp, vp, u64, vp, u64, u64, u64, vp], i32),
     ("orcg_boolrle_decode_device", [vp, vp, u64, vp, u64, u64, u64, vp], i32),
@@ -91,6 +95,51 @@ SIGNATURES = [
 ]
 
 _lib = None
+
+
+
+class TypeInfo(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint32), ("num_subtypes", ctypes.c_uint32), ("maximum_length", ctypes.c_uint32),
+                ("precision", ctypes.c_uint32), ("scale", ctypes.c_uint32)]
+
+
+class StripeInfo(ctypes.Structure):
+    _fields_ = [("offset", u64), ("index_length", u64), ("data_length", u64), ("footer_length", u64),
+                ("num_rows", u64)]
+
+
+class ColumnView(ctypes.Structure):
+    _fields_ = [("type_id", ctypes.c_uint32), ("kind", ctypes.c_uint32), ("encoding", ctypes.c_uint32),
+                ("decoded", ctypes.c_uint32), ("num_elements", u64), ("has_nulls", i32), ("not_null", vp),
+                ("data", vp), ("length", vp), ("offsets", vp), ("blob", vp), ("blob_len", u64)]
+
+
+u32 = ctypes.c_uint32
+# include/orcg_reader.h
+SIGNATURES += [
+    ("orcg_reader_open", [vp, vp, u64, ctypes.POINTER(vp)], i32),
+    ("orcg_reader_open_file", [vp, cp, ctypes.POINTER(vp)], i32),
+    ("orcg_reader_open_error", [], cp),
+    ("orcg_reader_destroy", [vp], None),
+    ("orcg_reader_last_error", [vp], cp),
+    ("orcg_reader_num_rows", [vp], u64),
+    ("orcg_reader_num_stripes", [vp], u64),
+    ("orcg_reader_row_index_stride", [vp], u32),
+    ("orcg_reader_compression", [vp], u32),
+    ("orcg_reader_compression_block_size", [vp], u64),
+    ("orcg_reader_format_version", [vp, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
+    ("orcg_reader_writer_version", [vp], u32),
+    ("orcg_reader_num_types", [vp], u32),
+    ("orcg_reader_type", [vp, u32, ctypes.POINTER(TypeInfo)], i32),
+    ("orcg_reader_subtypes", [vp, u32, ctypes.POINTER(u32), u32], i32),
+    ("orcg_reader_field_name", [vp, u32, u32], cp),
+    ("orcg_reader_stripe", [vp, u64, ctypes.POINTER(StripeInfo)], i32),
+    ("orcg_reader_select", [vp, vp, u32], i32),
+    ("orcg_reader_read_stripe", [vp, u64], i32),
+    ("orcg_reader_column", [vp, u32, ctypes.POINTER(ColumnView)], i32),
+    ("orcg_reader_copy_to_host", [vp, vp, vp, u64], i32),
+    ("orcg_reader_last_timings", [vp, ctypes.POINTER(ctypes.c_double)], i32),
+]
 
 
 def load():

@@ -10,8 +10,9 @@ OUT = os.path.join(HERE, "liborcgpu.so")
 OBJ = os.path.join(HERE, "build")
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "byterle_kernels.hip", "column_kernels.hip", "orcg_api.cpp", "byterle_api.cpp", "encoder.cpp"]
-HEADERS = ["orcg_internal.hh", "rlev2_device.hh", os.path.join("..", "..", "include", "orcg.h")]
+SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "encoder.cpp"]
+HEADERS = ["orcg_internal.hh", "rlev2_device.hh", "orc_file.hh", os.path.join("..", "..", "include", "orcg.h"),
+           os.path.join("..", "..", "include", "orcg_reader.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value"]
@@ -40,7 +41,7 @@ def build(force=False, verbose=False):
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
     if force or _mtime(OUT) < max(_mtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", "-fPIC", "-o", OUT] + objs + ["-Wl,-soname,liborcgpu.so"]
+        cmd = [HIPCC, "-shared", "-fPIC", "-o", OUT] + objs + ["-Wl,-soname,liborcgpu.so", "-lz", "-ldl", "-lpthread"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

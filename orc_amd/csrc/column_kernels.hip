@@ -150,6 +150,101 @@ __global__ __launch_bounds__(1024) void lengths_scan_kernel(const int64_t* __res
   if (threadIdx.x == 0) offsets[n] = (int64_t)carry_s;
 }
 
+// Multi-workgroup exclusive scan of int64 values (lengths -> offsets):
+// per-tile sums, one-workgroup scan of the sums, per-tile scan. Used for
+// direct string lengths (DATA offsets, StringDirectColumnReader::next,
+// c++/src/ColumnReader.cc:725-793) and list/map lengths (ListColumnReader::
+// nextInternal, :960-993) where the value count is the stripe's row count.
+constexpr int kScanTile = 4096;  // 256 threads x 16 values
+
+__global__ __launch_bounds__(kThreads) void tile_sum_kernel(const int64_t* __restrict__ in, uint64_t n,
+                                                             uint64_t* __restrict__ sums) {
+  __shared__ uint64_t red[kThreads / kWave];
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16u;
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (i0 + k < n) s += (uint64_t)in[i0 + k];
+  s = wave_inclusive_scan(s);
+  const int lane = threadIdx.x % kWave;
+  if (lane == kWave - 1) red[threadIdx.x / kWave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int w = 0; w < kThreads / kWave; ++w) t += red[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of `n` uint64 into `offsets` (n + 1 entries), one workgroup.
+__global__ __launch_bounds__(1024) void scan64_kernel(const uint64_t* __restrict__ in, uint64_t n,
+                                                       uint64_t* __restrict__ offsets) {
+  __shared__ uint64_t wsum[1024 / kWave];
+  __shared__ uint64_t carry_s;
+  const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (uint64_t b = 0; b < n; b += 1024) {
+    const uint64_t i = b + threadIdx.x;
+    const uint64_t x = i < n ? in[i] : 0;
+    const uint64_t inc = wave_inclusive_scan(x);
+    if (lane == kWave - 1) wsum[wv] = inc;
+    __syncthreads();
+    uint64_t before = carry_s;
+    for (int w = 0; w < wv; ++w) before += wsum[w];
+    if (i < n) offsets[i] = before + inc - x;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry_s = before + inc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) offsets[n] = carry_s;
+}
+
+__global__ __launch_bounds__(kThreads) void tile_scan_kernel(const int64_t* __restrict__ in, uint64_t n,
+                                                              const uint64_t* __restrict__ tile_off,
+                                                              int64_t* __restrict__ out) {
+  __shared__ uint64_t wsum[kThreads / kWave];
+  const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16u;
+  int64_t v[16];
+  uint64_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = i0 + k < n ? in[i0 + k] : 0;
+    s += (uint64_t)v[k];
+  }
+  const uint64_t inc = wave_inclusive_scan(s);
+  if (lane == kWave - 1) wsum[wv] = inc;
+  __syncthreads();
+  uint64_t run = tile_off[blockIdx.x] + inc - s;
+  for (int w = 0; w < wv; ++w) run += wsum[w];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (i0 + k < n) out[i0 + k] = (int64_t)run;
+    run += (uint64_t)v[k];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = (int64_t)tile_off[gridDim.x];
+}
+
+// Element conversions into the reference's batch types (LongVectorBatch /
+// DoubleVectorBatch): tinyint sign-extension (ByteColumnReader, c++/src/
+// ColumnReader.cc:188-223), boolean 0/1 (BooleanColumnReader :131-186),
+// float -> double (DoubleColumnReader<FLOAT> :359-450).
+template <typename Tin, typename Tout>
+__global__ void widen_kernel(const Tin* __restrict__ in, uint64_t n, Tout* __restrict__ out) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = (Tout)in[i];
+}
+
+// Flags any negative dictionary entry length (loadStringDictionary's check,
+// c++/src/DictionaryLoader.cc:71-77).
+__global__ void flag_negative_kernel(const int64_t* __restrict__ v, uint64_t n, unsigned long long* flag) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  bool neg = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) neg |= v[i] < 0;
+  if (__any(neg) && (threadIdx.x % kWave) == 0) atomicOr(flag, 1ull);
+}
+
 }  // namespace
 
 int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,
@@ -203,6 +298,76 @@ int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t
   else
     return set_error(ctx, ORCG_INVALID_ARGUMENT, "index width must be 8 or 4");
   return hip_check(ctx, hipGetLastError(), "dictionary gather launch");
+}
+
+}  // namespace orcg
+
+namespace orcg {
+
+int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out) {
+  if (n == 0) {
+    return hip_check(ctx, hipMemsetAsync(d_out, 0, sizeof(int64_t), ctx->stream), "scan memset");
+  }
+  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many values");
+  void* d_sums;
+  int rc = scratch(ctx, 7, (2 * tiles + 1) * sizeof(uint64_t), &d_sums);
+  if (rc) return rc;
+  uint64_t* sums = (uint64_t*)d_sums;
+  uint64_t* toff = sums + tiles;
+  hipLaunchKernelGGL(tile_sum_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n, sums);
+  hipLaunchKernelGGL(scan64_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const uint64_t*)sums, tiles, toff);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n,
+                     (const uint64_t*)toff, d_out);
+  return hip_check(ctx, hipGetLastError(), "scan launch");
+}
+
+int launch_count_nonzero(Ctx* ctx, const uint8_t* d_nn, uint64_t n, uint64_t* d_total) {
+  if (n == 0) return hip_check(ctx, hipMemsetAsync(d_total, 0, sizeof(uint64_t), ctx->stream), "count memset");
+  const uint64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many rows");
+  void *d_counts, *d_off;
+  int rc = scratch(ctx, 5, tiles * sizeof(uint32_t), &d_counts);
+  if (!rc) rc = scratch(ctx, 6, (tiles + 1) * sizeof(uint64_t), &d_off);
+  if (rc) return rc;
+  hipLaunchKernelGGL(tile_count_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_nn, n,
+                     (uint32_t*)d_counts);
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const uint32_t*)d_counts, tiles,
+                     (uint64_t*)d_off);
+  rc = hip_check(ctx, hipMemcpyAsync(d_total, (uint64_t*)d_off + tiles, sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                                     ctx->stream), "count copy");
+  return rc ? rc : hip_check(ctx, hipGetLastError(), "count launch");
+}
+
+int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_flag) {
+  int rc = hip_check(ctx, hipMemsetAsync(d_flag, 0, sizeof(uint64_t), ctx->stream), "flag memset");
+  if (rc || n == 0) return rc;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(flag_negative_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_v, n,
+                     (unsigned long long*)d_flag);
+  return hip_check(ctx, hipGetLastError(), "flag launch");
+}
+
+int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out) {
+  if (n == 0) return ORCG_OK;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256 * 32);
+  switch (kind) {
+    case kWidenI8:
+      hipLaunchKernelGGL((widen_kernel<int8_t, int64_t>), dim3(grid), dim3(256), 0, ctx->stream,
+                         (const int8_t*)d_in, n, (int64_t*)d_out);
+      break;
+    case kWidenU8:
+      hipLaunchKernelGGL((widen_kernel<uint8_t, int64_t>), dim3(grid), dim3(256), 0, ctx->stream,
+                         (const uint8_t*)d_in, n, (int64_t*)d_out);
+      break;
+    case kWidenF32:
+      hipLaunchKernelGGL((widen_kernel<float, double>), dim3(grid), dim3(256), 0, ctx->stream, (const float*)d_in,
+                         n, (double*)d_out);
+      break;
+    default:
+      return set_error(ctx, ORCG_INVALID_ARGUMENT, "bad widen kind");
+  }
+  return hip_check(ctx, hipGetLastError(), "widen launch");
 }
 
 }  // namespace orcg

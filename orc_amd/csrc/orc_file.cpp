@@ -1,0 +1,391 @@
+// ORC tail / stripe-footer parsing and block decompression (see orc_file.hh).
+#include "orc_file.hh"
+
+#include <dlfcn.h>
+#include <string.h>
+#include <zlib.h>
+
+
+namespace orcg {
+namespace file {
+namespace {
+
+// Protocol-buffers wire format: (field << 3 | wire type) keys, base-128
+// varints, 64/32-bit little-endian fixed fields, length-delimited bytes.
+struct Pb {
+  const uint8_t* p;
+  const uint8_t* end;
+  bool ok = true;
+  Pb(const uint8_t* b, uint64_t n) : p(b), end(b + n) {}
+  bool more() const { return ok && p < end; }
+  uint64_t varint() {
+    uint64_t r = 0;
+    for (int sh = 0; sh < 70; sh += 7) {
+      if (p >= end) {
+        ok = false;
+        return 0;
+      }
+      const uint8_t b = *p++;
+      if (sh < 64) r |= (uint64_t)(b & 0x7f) << sh;
+      if (!(b & 0x80)) return r;
+    }
+    ok = false;
+    return 0;
+  }
+  bool key(uint32_t& field, uint32_t& wire) {
+    const uint64_t k = varint();
+    field = (uint32_t)(k >> 3);
+    wire = (uint32_t)(k & 7);
+    return ok;
+  }
+  Pb bytes() {
+    const uint64_t n = varint();
+    if (!ok || n > (uint64_t)(end - p)) {
+      ok = false;
+      return Pb(p, 0);
+    }
+    Pb sub(p, n);
+    p += n;
+    return sub;
+  }
+  void skip(uint32_t wire) {
+    switch (wire) {
+      case 0: varint(); break;
+      case 1: if (end - p < 8) ok = false; else p += 8; break;
+      case 2: bytes(); break;
+      case 5: if (end - p < 4) ok = false; else p += 4; break;
+      default: ok = false;
+    }
+  }
+  std::string str() {
+    Pb s = bytes();
+    return std::string((const char*)s.p, (size_t)(s.end - s.p));
+  }
+  // repeated uint32, packed (wire 2) or not (wire 0)
+  void u32s(uint32_t wire, std::vector<uint32_t>& out) {
+    if (wire == 2) {
+      Pb s = bytes();
+      while (s.more()) out.push_back((uint32_t)s.varint());
+      if (!s.ok) ok = false;
+    } else if (wire == 0) {
+      out.push_back((uint32_t)varint());
+    } else {
+      ok = false;
+    }
+  }
+};
+
+bool parse_stripe_info(Pb m, StripeInfo& s) {
+  uint32_t f, w;
+  while (m.more() && m.key(f, w)) {
+    if (w == 0 && f >= 1 && f <= 5) {
+      const uint64_t v = m.varint();
+      if (f == 1) s.offset = v;
+      else if (f == 2) s.index_length = v;
+      else if (f == 3) s.data_length = v;
+      else if (f == 4) s.footer_length = v;
+      else s.num_rows = v;
+    } else {
+      m.skip(w);
+    }
+  }
+  return m.ok;
+}
+
+bool parse_type(Pb m, TypeInfo& t) {
+  uint32_t f, w;
+  while (m.more() && m.key(f, w)) {
+    if (f == 1 && w == 0) t.kind = (uint32_t)m.varint();
+    else if (f == 2) m.u32s(w, t.subtypes);
+    else if (f == 3 && w == 2) t.field_names.push_back(m.str());
+    else if (f == 4 && w == 0) t.maximum_length = (uint32_t)m.varint();
+    else if (f == 5 && w == 0) t.precision = (uint32_t)m.varint();
+    else if (f == 6 && w == 0) t.scale = (uint32_t)m.varint();
+    else m.skip(w);
+  }
+  return m.ok;
+}
+
+// ---- snappy (raw block format) -------------------------------------------
+// The reference links libsnappy (SnappyDecompressionStream, Compression.cc);
+// this is the published block format: a varint uncompressed length, then
+// literal / copy elements selected by the low two tag bits.
+bool snappy_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t& out_len,
+                       std::string& err) {
+  const uint8_t* p = in;
+  const uint8_t* end = in + n;
+  uint64_t ulen = 0;
+  for (int sh = 0;; sh += 7) {
+    if (p >= end || sh > 35) { err = "snappy: bad length"; return false; }
+    const uint8_t b = *p++;
+    ulen |= (uint64_t)(b & 0x7f) << sh;
+    if (!(b & 0x80)) break;
+  }
+  if (ulen > cap) { err = "snappy: output exceeds the compression block size"; return false; }
+  uint64_t o = 0;
+  while (p < end) {
+    const uint8_t tag = *p++;
+    const uint32_t kind = tag & 3u;
+    if (kind == 0) {
+      uint64_t len = (tag >> 2) + 1u;
+      if (len > 60) {
+        const uint32_t nb = (uint32_t)len - 60;
+        if ((uint64_t)(end - p) < nb) { err = "snappy: truncated literal"; return false; }
+        len = 0;
+        for (uint32_t i = 0; i < nb; ++i) len |= (uint64_t)p[i] << (8 * i);
+        len += 1;
+        p += nb;
+      }
+      if ((uint64_t)(end - p) < len || o + len > ulen) { err = "snappy: literal out of range"; return false; }
+      memcpy(out + o, p, len);
+      p += len;
+      o += len;
+    } else {
+      uint64_t len, off;
+      if (kind == 1) {
+        if (p >= end) { err = "snappy: truncated copy"; return false; }
+        len = 4 + ((tag >> 2) & 7u);
+        off = ((uint64_t)(tag >> 5) << 8) | *p++;
+      } else if (kind == 2) {
+        if (end - p < 2) { err = "snappy: truncated copy"; return false; }
+        len = 1 + (tag >> 2);
+        off = (uint64_t)p[0] | ((uint64_t)p[1] << 8);
+        p += 2;
+      } else {
+        if (end - p < 4) { err = "snappy: truncated copy"; return false; }
+        len = 1 + (tag >> 2);
+        off = (uint64_t)p[0] | ((uint64_t)p[1] << 8) | ((uint64_t)p[2] << 16) | ((uint64_t)p[3] << 24);
+        p += 4;
+      }
+      if (off == 0 || off > o || o + len > ulen) { err = "snappy: copy out of range"; return false; }
+      uint8_t* d = out + o;
+      const uint8_t* s = d - off;
+      if (off >= len) memcpy(d, s, len);
+      else for (uint64_t i = 0; i < len; ++i) d[i] = s[i];  // overlapping copy
+      o += len;
+    }
+  }
+  if (o != ulen) { err = "snappy: length mismatch"; return false; }
+  out_len = o;
+  return true;
+}
+
+// ---- lz4 / zstd through the system libraries (dlopen) ----------------------
+// The reference links liblz4 (LZ4_decompress_safe, Compression.cc Lz4
+// DecompressionStream) and libzstd (ZSTD_decompressDCtx). Only the runtime
+// .so files are in this image; the two entry points are resolved at run time.
+typedef int (*lz4_fn)(const char*, char*, int, int);
+typedef size_t (*zstd_fn)(void*, size_t, const void*, size_t);
+typedef unsigned (*zstd_err_fn)(size_t);
+
+struct DynCodecs {
+  lz4_fn lz4 = nullptr;
+  zstd_fn zstd = nullptr;
+  zstd_err_fn zstd_is_error = nullptr;
+  DynCodecs() {
+    if (void* h = dlopen("liblz4.so.1", RTLD_NOW | RTLD_LOCAL)) lz4 = (lz4_fn)dlsym(h, "LZ4_decompress_safe");
+    if (void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL)) {
+      zstd = (zstd_fn)dlsym(h, "ZSTD_decompress");
+      zstd_is_error = (zstd_err_fn)dlsym(h, "ZSTD_isError");
+    }
+  }
+};
+
+const DynCodecs& codecs() {
+  static DynCodecs c;
+  return c;
+}
+
+}  // namespace
+
+const char* compression_name(uint32_t c) {
+  switch (c) {
+    case kNone: return "none";
+    case kZlib: return "zlib";
+    case kSnappy: return "snappy";
+    case kLzo: return "lzo";
+    case kLz4: return "lz4";
+    case kZstd: return "zstd";
+  }
+  return "unknown";
+}
+
+bool parse_postscript(const uint8_t* p, uint64_t n, PostScript& ps) {
+  Pb m(p, n);
+  uint32_t f, w;
+  while (m.more() && m.key(f, w)) {
+    if (f == 1 && w == 0) ps.footer_length = m.varint();
+    else if (f == 2 && w == 0) ps.compression = (uint32_t)m.varint();
+    else if (f == 3 && w == 0) ps.block_size = m.varint();
+    else if (f == 4) m.u32s(w, ps.version);
+    else if (f == 5 && w == 0) ps.metadata_length = m.varint();
+    else if (f == 6 && w == 0) ps.writer_version = (uint32_t)m.varint();
+    else if (f == 8000 && w == 2) ps.magic = m.str();
+    else m.skip(w);
+  }
+  return m.ok;
+}
+
+bool parse_footer(const uint8_t* p, uint64_t n, Footer& ft) {
+  Pb m(p, n);
+  uint32_t f, w;
+  while (m.more() && m.key(f, w)) {
+    if (f == 1 && w == 0) ft.header_length = m.varint();
+    else if (f == 2 && w == 0) ft.content_length = m.varint();
+    else if (f == 3 && w == 2) {
+      ft.stripes.emplace_back();
+      if (!parse_stripe_info(m.bytes(), ft.stripes.back())) return false;
+    } else if (f == 4 && w == 2) {
+      ft.types.emplace_back();
+      if (!parse_type(m.bytes(), ft.types.back())) return false;
+    } else if (f == 6 && w == 0) ft.num_rows = m.varint();
+    else if (f == 8 && w == 0) ft.row_index_stride = (uint32_t)m.varint();
+    else if (f == 9 && w == 0) ft.writer = (uint32_t)m.varint();
+    else m.skip(w);
+  }
+  return m.ok;
+}
+
+bool parse_stripe_footer(const uint8_t* p, uint64_t n, uint64_t stripe_offset, StripeFooter& sf) {
+  Pb m(p, n);
+  uint32_t f, w;
+  uint64_t off = stripe_offset;
+  while (m.more() && m.key(f, w)) {
+    if (f == 1 && w == 2) {
+      Pb s = m.bytes();
+      StreamInfo si;
+      uint32_t g, v;
+      while (s.more() && s.key(g, v)) {
+        if (g == 1 && v == 0) si.kind = (uint32_t)s.varint();
+        else if (g == 2 && v == 0) si.column = (uint32_t)s.varint();
+        else if (g == 3 && v == 0) si.length = s.varint();
+        else s.skip(v);
+      }
+      if (!s.ok) return false;
+      si.offset = off;  // streams are laid out back to back in footer order
+      off += si.length;
+      sf.streams.push_back(si);
+    } else if (f == 2 && w == 2) {
+      Pb s = m.bytes();
+      ColumnEncoding ce;
+      uint32_t g, v;
+      while (s.more() && s.key(g, v)) {
+        if (g == 1 && v == 0) ce.kind = (uint32_t)s.varint();
+        else if (g == 2 && v == 0) ce.dictionary_size = (uint32_t)s.varint();
+        else s.skip(v);
+      }
+      if (!s.ok) return false;
+      sf.encodings.push_back(ce);
+    } else if (f == 3 && w == 2) {
+      sf.writer_timezone = m.str();
+    } else {
+      m.skip(w);
+    }
+  }
+  return m.ok;
+}
+
+bool split_chunks(const uint8_t* file, uint64_t off, uint64_t len, uint32_t compression, std::vector<Chunk>& out,
+                  std::string& err) {
+  if (compression == kNone) {
+    Chunk c;
+    c.src_off = off;
+    c.src_len = len;
+    c.original = true;
+    out.push_back(c);
+    return true;
+  }
+  uint64_t p = off;
+  const uint64_t end = off + len;
+  while (p < end) {
+    if (end - p < 3) {
+      err = "Read past EOF in DecompressionStream::readBuffer";
+      return false;
+    }
+    const uint32_t h = (uint32_t)file[p] | ((uint32_t)file[p + 1] << 8) | ((uint32_t)file[p + 2] << 16);
+    Chunk c;
+    c.original = (h & 1u) != 0;
+    c.src_len = h >> 1;
+    c.src_off = p + 3;
+    if (c.src_len > end - c.src_off) {
+      err = "Read past EOF in DecompressionStream::readBuffer";
+      return false;
+    }
+    out.push_back(c);
+    p = c.src_off + c.src_len;
+  }
+  return true;
+}
+
+bool decompress_chunk(uint32_t compression, const uint8_t* file, Chunk& c, uint8_t* dst, uint64_t cap,
+                      std::string& err) {
+  const uint8_t* in = file + c.src_off;
+  if (c.original) {
+    if (c.src_len > cap) { err = "chunk larger than the compression block size"; return false; }
+    memcpy(dst, in, c.src_len);
+    c.dst_len = c.src_len;
+    return true;
+  }
+  switch (compression) {
+    case kZlib: {
+      // raw deflate (inflateInit2 with -15 window bits), ZlibDecompressionStream
+      z_stream zs;
+      memset(&zs, 0, sizeof(zs));
+      if (inflateInit2(&zs, -15) != Z_OK) { err = "Failed to initialize inflate"; return false; }
+      zs.next_in = const_cast<Bytef*>(in);
+      zs.avail_in = (uInt)c.src_len;
+      zs.next_out = dst;
+      zs.avail_out = (uInt)cap;
+      const int r = inflate(&zs, Z_FINISH);
+      c.dst_len = cap - zs.avail_out;
+      inflateEnd(&zs);
+      if (r != Z_STREAM_END) {
+        err = r == Z_BUF_ERROR ? "Buffer error in ZlibDecompressionStream::NextDecompress"
+                               : "Failed to inflate input data in ZlibDecompressionStream";
+        return false;
+      }
+      return true;
+    }
+    case kSnappy:
+      return snappy_decompress(in, c.src_len, dst, cap, c.dst_len, err);
+    case kLz4: {
+      const auto& k = codecs();
+      if (!k.lz4) { err = "lz4 codec library (liblz4.so.1) not available"; return false; }
+      const int r = k.lz4((const char*)in, (char*)dst, (int)c.src_len, (int)cap);
+      if (r < 0) { err = "Corrupt lz4 compressed block"; return false; }
+      c.dst_len = (uint64_t)r;
+      return true;
+    }
+    case kZstd: {
+      const auto& k = codecs();
+      if (!k.zstd) { err = "zstd codec library (libzstd.so.1) not available"; return false; }
+      const size_t r = k.zstd(dst, cap, in, c.src_len);
+      if (k.zstd_is_error(r)) { err = "Corrupt zstd compressed block"; return false; }
+      c.dst_len = r;
+      return true;
+    }
+    case kLzo:
+      err = "LZO compression is not supported by the GPU reader";
+      return false;
+  }
+  err = "Unknown compression type";
+  return false;
+}
+
+bool read_range(const uint8_t* file, uint64_t off, uint64_t len, uint32_t compression, uint64_t block_size,
+                std::vector<uint8_t>& out, std::string& err) {
+  std::vector<Chunk> chunks;
+  if (!split_chunks(file, off, len, compression, chunks, err)) return false;
+  out.clear();
+  for (auto& c : chunks) {
+    const uint64_t at = out.size();
+    const uint64_t cap = c.original ? c.src_len : block_size;
+    out.resize(at + cap);
+    if (!decompress_chunk(compression, file, c, out.data() + at, cap, err)) return false;
+    out.resize(at + c.dst_len);
+  }
+  return true;
+}
+
+}  // namespace file
+}  // namespace orcg

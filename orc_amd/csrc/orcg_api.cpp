@@ -22,6 +22,7 @@ const char* dev_error_message(uint32_t code) {
     case kErrBadSegment: return "Stream position is not at a run boundary";
     case kErrByteBadRead: return "bad read in nextBuffer";
     case kErrDictIndex: return "Entry index out of range in StringDictionaryColumn";
+    case kErrV1BadRead: return "bad read in readByte";
   }
   return "unknown device error";
 }

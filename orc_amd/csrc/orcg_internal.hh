@@ -23,6 +23,7 @@ enum DevErr : uint32_t {
   kErrBadSegment = 5,      // positions / segment table not run aligned (InvalidArgument)
   kErrByteBadRead = 6,     // "bad read in nextBuffer" (ByteRLE.cc:364)
   kErrDictIndex = 7,       // "Entry index out of range in StringDictionaryColumn" (ColumnReader.cc:578)
+  kErrV1BadRead = 8,       // "bad read in readByte" (RLEv1.cc:141-146)
 };
 
 const char* dev_error_message(uint32_t code);
@@ -68,11 +69,22 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
 
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
                    bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst);
+int launch_rlev1(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed, const uint64_t* d_segtab,
+                 uint64_t nsegs, uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes);
 int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,
                    int fill_mode, int64_t fill);
 int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets);
 int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t* d_nn, uint64_t n,
                        const int64_t* d_offsets, uint64_t dict_size, int64_t* d_start, int64_t* d_len);
+
+// Multi-workgroup exclusive scan: d_out[0..n] (n + 1 entries). Scratch 7.
+int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out);
+// Number of non-zero bytes of d_nn[0..n) into *d_total (device). Scratch 5, 6.
+int launch_count_nonzero(Ctx* ctx, const uint8_t* d_nn, uint64_t n, uint64_t* d_total);
+// *d_flag = 1 if any d_v[i] < 0, else 0.
+int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_flag);
+enum WidenKind { kWidenI8 = 0, kWidenU8 = 1, kWidenF32 = 2 };
+int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out);
 
 // Dispatch on ctx->rlev2_variant.
 inline int launch_rlev2(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
@@ -100,6 +112,7 @@ struct orcg_rlev2_plan {
 };
 
 orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
+orcg_rlev2_plan* make_v1_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
 orcg_rlev2_plan* make_byte_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
 // H2D + RLEv2 decode of the first `count` values + D2H into host `out`.
 int decode_host_dense(orcg::Ctx* c, const uint8_t* src, uint64_t len, int is_signed,

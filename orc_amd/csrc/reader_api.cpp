@@ -1,0 +1,800 @@
+// File-level reader (include/orcg_reader.h): ORC tail -> stripe streams ->
+// host decompression -> one H2D per stripe -> HIP decode of every selected
+// column into device batches.
+//
+// Column semantics follow the reference's column readers
+// (c++/src/ColumnReader.cc): ColumnReader::next's PRESENT handling with the
+// parent's incoming mask (:81-104; a child's PRESENT stream has bits only for
+// the parent's non-null rows), IntegerColumnReader (:225-258),
+// BooleanColumnReader (:131-186), ByteColumnReader (:188-223),
+// DoubleColumnReader (:359-450), StringDictionaryColumnReader (:509-607),
+// StringDirectColumnReader (:615-793), StructColumnReader (:795-880),
+// ListColumnReader / MapColumnReader (:882-1157). Encodings pick RLE v1 or v2
+// (createRleDecoder, c++/src/RLE.cc:48-60 via ColumnReader.cc
+// convertRleVersion).
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <thread>
+
+#include "../../include/orcg_reader.h"
+#include "orc_file.hh"
+#include "orcg_internal.hh"
+
+using namespace orcg;
+using namespace orcg::file;
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+unsigned host_threads() {
+  if (const char* e = getenv("ORCG_HOST_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return (unsigned)v;
+  }
+  const unsigned hc = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(16u, hc ? hc : 1u));
+}
+
+template <typename F>
+void parallel_for(size_t n, F&& f) {
+  const unsigned nt = (unsigned)std::min<size_t>(host_threads(), n);
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> ts;
+  for (unsigned t = 0; t < nt; ++t)
+    ts.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+    });
+  for (auto& t : ts) t.join();
+}
+
+bool is_string_kind(uint32_t k) {
+  return k == ORCG_TYPE_STRING || k == ORCG_TYPE_VARCHAR || k == ORCG_TYPE_CHAR || k == ORCG_TYPE_BINARY;
+}
+bool is_int_kind(uint32_t k) {
+  return k == ORCG_TYPE_SHORT || k == ORCG_TYPE_INT || k == ORCG_TYPE_LONG || k == ORCG_TYPE_DATE;
+}
+bool is_supported(uint32_t k) {
+  return k != ORCG_TYPE_TIMESTAMP && k != ORCG_TYPE_UNION && k != ORCG_TYPE_DECIMAL &&
+         k != ORCG_TYPE_TIMESTAMP_INSTANT && k <= ORCG_TYPE_CHAR;
+}
+
+// Caching device allocator: blocks are recycled stripe to stripe.
+struct DevPool {
+  int device = 0;
+  std::multimap<size_t, void*> free_blocks;
+  std::vector<std::pair<void*, size_t>> used;
+  ~DevPool() {
+    release_all();
+    for (auto& kv : free_blocks) (void)hipFree(kv.second);
+  }
+  void release_all() {
+    for (auto& u : used) free_blocks.emplace(u.second, u.first);
+    used.clear();
+  }
+  void* get(size_t bytes) {
+    bytes = std::max<size_t>(256, (bytes + 255) & ~(size_t)255);
+    auto it = free_blocks.lower_bound(bytes);
+    if (it != free_blocks.end() && it->first <= 2 * bytes + (1 << 20)) {
+      void* p = it->second;
+      const size_t sz = it->first;
+      free_blocks.erase(it);
+      used.emplace_back(p, sz);
+      return p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      // drop cached blocks and retry once
+      for (auto& kv : free_blocks) (void)hipFree(kv.second);
+      free_blocks.clear();
+      if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    }
+    used.emplace_back(p, bytes);
+    return p;
+  }
+};
+
+struct StreamBuf {
+  bool present = false;
+  uint64_t host_off = 0;  // offset in staging (== device offset)
+  uint64_t len = 0;       // decompressed bytes
+  std::unique_ptr<orcg_rlev2_plan> plan;
+  uint64_t seg_off = 0;   // offset of the plan's segment table in staging
+};
+
+struct Col {
+  bool selected = true, decoded = false;
+  uint32_t kind = 0, encoding = 0;
+  uint64_t n = 0;
+  bool has_nulls = false;
+  uint8_t* nn = nullptr;
+  void* data = nullptr;
+  int64_t* length = nullptr;
+  int64_t* offsets = nullptr;
+  uint8_t* blob = nullptr;
+  uint64_t blob_len = 0;
+  uint64_t dict_size = 0;  // ColumnEncoding.dictionarySize of this stripe
+  StreamBuf s[4];  // PRESENT, DATA, LENGTH, DICTIONARY_DATA
+};
+
+enum { kSlotPresent = 0, kSlotData = 1, kSlotLength = 2, kSlotDict = 3 };
+
+int slot_of(uint32_t stream_kind) {
+  switch (stream_kind) {
+    case kPresent: return kSlotPresent;
+    case kData: return kSlotData;
+    case kLength: return kSlotLength;
+    case kDictionaryData: return kSlotDict;
+  }
+  return -1;
+}
+
+}  // namespace
+
+struct orcg_reader {
+  Ctx* ctx = nullptr;
+  const uint8_t* file = nullptr;
+  uint64_t file_len = 0;
+  void* mapped = nullptr;
+  PostScript ps;
+  Footer footer;
+  std::vector<Col> cols;
+  std::string last_error;
+  DevPool pool;
+  uint8_t* h_stage = nullptr;  // pinned staging
+  size_t h_cap = 0;
+  uint8_t* d_stage = nullptr;  // device copy of the staging buffer
+  uint64_t* d_scalars = nullptr;
+  double timings[4] = {0, 0, 0, 0};
+
+  ~orcg_reader() {
+    if (h_stage) (void)hipHostFree(h_stage);
+    if (mapped) munmap(mapped, file_len);
+  }
+  int fail(int status, const std::string& m) {
+    last_error = m;
+    if (ctx) ctx->last_error = m;
+    return status;
+  }
+  int fail_ctx(int rc) { return fail(rc, ctx ? ctx->last_error : std::string("device error")); }
+
+  int open_tail();
+  int read_stripe(uint64_t s);
+  int decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count);
+  int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out);
+  int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out);
+  int nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out);
+  int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
+  template <typename T>
+  T* alloc(uint64_t count) {
+    return (T*)pool.get(std::max<uint64_t>(count, 1) * sizeof(T));
+  }
+};
+
+int orcg_reader::open_tail() {
+  // ReaderImpl tail read (c++/src/Reader.cc:1650-1700, readPostscript :1548-1567)
+  if (file_len < 4) return fail(ORCG_PARSE_ERROR, "File size too small");
+  const uint64_t ps_len = file[file_len - 1];
+  if (ps_len < 3) return fail(ORCG_PARSE_ERROR, "Invalid ORC postscript length");
+  if (memcmp(file + file_len - 1 - 3, "ORC", 3) != 0 && memcmp(file, "ORC", 3) != 0)
+    return fail(ORCG_PARSE_ERROR, "Not an ORC file");
+  if (file_len < 1 + ps_len)
+    return fail(ORCG_PARSE_ERROR, "Invalid ORC postscript length: " + std::to_string(ps_len) +
+                                      ", file length = " + std::to_string(file_len));
+  if (!parse_postscript(file + file_len - 1 - ps_len, ps_len, ps))
+    return fail(ORCG_PARSE_ERROR, "Failed to parse the postscript");
+  if (ps.block_size == 0) ps.block_size = 256 * 1024;
+  const uint64_t tail = 1 + ps_len + ps.footer_length;
+  if (tail >= file_len)
+    return fail(ORCG_PARSE_ERROR, "Invalid tail size: footerSize=" + std::to_string(ps.footer_length) +
+                                      ", postscriptLength=" + std::to_string(ps_len) +
+                                      ", fileLength=" + std::to_string(file_len));
+  if (ps.compression > kZstd) return fail(ORCG_PARSE_ERROR, "Unknown compression type");
+  std::vector<uint8_t> fbytes;
+  std::string err;
+  if (!read_range(file, file_len - tail, ps.footer_length, ps.compression, ps.block_size, fbytes, err))
+    return fail(ORCG_PARSE_ERROR, err);
+  if (!parse_footer(fbytes.data(), fbytes.size(), footer)) return fail(ORCG_PARSE_ERROR, "Failed to parse the footer");
+  // checkProtoTypes (Reader.cc:1575-1605)
+  const size_t nt = footer.types.size();
+  if (nt == 0) return fail(ORCG_PARSE_ERROR, "Footer is corrupt: no types found");
+  for (size_t i = 0; i < nt; ++i) {
+    const auto& t = footer.types[i];
+    if (t.kind == ORCG_TYPE_STRUCT && t.subtypes.size() != t.field_names.size())
+      return fail(ORCG_PARSE_ERROR, "Footer is corrupt: STRUCT type " + std::to_string(i) + " has " +
+                                        std::to_string(t.subtypes.size()) + " subTypes, but has " +
+                                        std::to_string(t.field_names.size()) + " fieldNames");
+    for (size_t j = 0; j < t.subtypes.size(); ++j) {
+      const uint32_t st = t.subtypes[j];
+      if (st <= i)
+        return fail(ORCG_PARSE_ERROR, "Footer is corrupt: malformed link from type " + std::to_string(i) +
+                                          " to " + std::to_string(st));
+      if (st >= nt) return fail(ORCG_PARSE_ERROR, "Footer is corrupt: types(" + std::to_string(st) + ") not exists");
+      if (j > 0 && t.subtypes[j - 1] >= st)
+        return fail(ORCG_PARSE_ERROR, "Footer is corrupt: subType(" + std::to_string(j - 1) + ") >= subType(" +
+                                          std::to_string(j) + ") in types(" + std::to_string(i) + ")");
+    }
+  }
+  cols = std::vector<Col>(nt);
+  for (size_t i = 0; i < nt; ++i) cols[i].kind = footer.types[i].kind;
+  return ORCG_OK;
+}
+
+int orcg_reader::nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out) {
+  int rc = launch_count_nonzero(ctx, nn, n, d_scalars);
+  if (!rc) rc = hip_check(ctx, hipMemcpyAsync(&out, d_scalars, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H count");
+  if (!rc) rc = sync_ctx(ctx);
+  return rc;
+}
+
+int orcg_reader::scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width) {
+  return launch_scatter(ctx, dense, nn, n, out, width, 1, 0);
+}
+
+int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out) {
+  StreamBuf& sb = c.s[slot];
+  if (count == 0) return ORCG_OK;
+  if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
+  if (count > sb.plan->values) {
+    const bool v1 = c.encoding == kDirect || c.encoding == kDictionary;
+    const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)(v1 ? kErrV1BadRead : kErrBadRead);
+    return fail(dev_error_status(e), dev_error_message(e));
+  }
+  const uint8_t* d_src = d_stage + sb.host_off;
+  const uint64_t* d_seg = (const uint64_t*)(d_stage + sb.seg_off);
+  const int sg = is_signed ? 1 : 0;
+  int rc;
+  if (c.encoding == kDirect || c.encoding == kDictionary)
+    rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, sb.plan->segs.size(), 0, count, out, 8);
+  else
+    rc = launch_rlev2(ctx, d_src, sb.len, sg, d_seg, sb.plan->segs.size(), false, 0, 0, count, out, 8);
+  return rc ? fail_ctx(rc) : ORCG_OK;
+}
+
+int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out) {
+  StreamBuf& sb = c.s[slot];
+  if (count == 0) return ORCG_OK;
+  if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
+  const uint64_t avail = boolean ? sb.plan->values * 8 : sb.plan->values;
+  if (count > avail) {
+    const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)kErrByteBadRead;
+    return fail(dev_error_status(e), dev_error_message(e));
+  }
+  const int rc = launch_byterle(ctx, d_stage + sb.host_off, sb.len, (const uint64_t*)(d_stage + sb.seg_off),
+                                sb.plan->segs.size(), boolean, 0, count, out);
+  return rc ? fail_ctx(rc) : ORCG_OK;
+}
+
+#define ORCG_ALLOC(T, v, count)                                                   \
+  T* v = alloc<T>(count);                                                         \
+  if (!v) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed")
+#define ORCG_ALLOC_TO(T, v, count)                                                \
+  v = alloc<T>(count);                                                            \
+  if (!v) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed")
+
+int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count) {
+  Col& c = cols[id];
+  if (!c.selected || !is_supported(c.kind)) return ORCG_OK;
+  c.n = n;
+  c.decoded = true;
+  int rc;
+  // ColumnReader::next: PRESENT bits for the incoming non-null rows
+  uint64_t nonnull = in_nn ? in_count : n;
+  uint8_t* nn = nullptr;
+  if (c.s[kSlotPresent].present) {
+    ORCG_ALLOC(uint8_t, bits, in_count + 8);
+    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits))) return rc;
+    if (in_nn) {
+      ORCG_ALLOC_TO(uint8_t, nn, n);
+      if ((rc = scatter(bits, in_nn, n, nn, 1))) return fail_ctx(rc);
+    } else {
+      nn = bits;
+    }
+    if ((rc = nonnull_count(nn, n, nonnull))) return fail_ctx(rc);
+  } else if (in_nn) {
+    nn = const_cast<uint8_t*>(in_nn);
+  }
+  c.has_nulls = nn != nullptr && nonnull < n;
+  if (in_nn && !c.s[kSlotPresent].present) c.has_nulls = true;  // incoming mask copied (:97-101)
+  c.nn = c.has_nulls ? nn : nullptr;
+  const uint8_t* row_nn = c.nn;
+
+  auto place_i64 = [&](int64_t* dense) -> int64_t* {
+    if (!row_nn) return dense;
+    int64_t* out = alloc<int64_t>(n);
+    if (!out) return nullptr;
+    return scatter(dense, row_nn, n, out, 8) ? nullptr : out;
+  };
+
+  const uint32_t k = c.kind;
+  const bool has_data = c.s[kSlotData].present, has_len = c.s[kSlotLength].present;
+  if (is_int_kind(k)) {
+    if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Integer column");
+    ORCG_ALLOC(int64_t, dense, nonnull);
+    if ((rc = int_stream(c, kSlotData, true, nonnull, dense))) return rc;
+    if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
+  } else if (k == ORCG_TYPE_BOOLEAN || k == ORCG_TYPE_BYTE) {
+    if (!has_data)
+      return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_BOOLEAN ? "DATA stream not found in Boolean column"
+                                                           : "DATA stream not found in Byte column");
+    ORCG_ALLOC(uint8_t, bytes, nonnull + 8);
+    if ((rc = byte_stream(c, kSlotData, k == ORCG_TYPE_BOOLEAN, nonnull, bytes))) return rc;
+    ORCG_ALLOC(int64_t, dense, nonnull);
+    if ((rc = launch_widen(ctx, bytes, k == ORCG_TYPE_BYTE ? kWidenI8 : kWidenU8, nonnull, dense))) return fail_ctx(rc);
+    if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
+  } else if (k == ORCG_TYPE_FLOAT || k == ORCG_TYPE_DOUBLE) {
+    if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Double column");
+    StreamBuf& sb = c.s[kSlotData];
+    const uint64_t w = k == ORCG_TYPE_FLOAT ? 4 : 8;
+    if (sb.len < w * nonnull) return fail(ORCG_PARSE_ERROR, "bad read in DoubleColumnReader::next()");
+    const void* raw = d_stage + sb.host_off;
+    double* dense;
+    if (k == ORCG_TYPE_FLOAT) {
+      ORCG_ALLOC_TO(double, dense, nonnull);
+      if ((rc = launch_widen(ctx, raw, kWidenF32, nonnull, dense))) return fail_ctx(rc);
+    } else {
+      dense = (double*)raw;  // zero copy: the stream bytes are the values
+    }
+    if (row_nn) {
+      ORCG_ALLOC(double, out, n);
+      if ((rc = scatter(dense, row_nn, n, out, 8))) return fail_ctx(rc);
+      c.data = out;
+    } else {
+      c.data = dense;
+    }
+  } else if (is_string_kind(k)) {
+    const bool dict = c.encoding == kDictionary || c.encoding == kDictionaryV2;
+    ORCG_ALLOC(int64_t, start, n);
+    ORCG_ALLOC(int64_t, len, n);
+    if (dict) {
+      // loadStringDictionary (DictionaryLoader.cc:43-97), then
+      // StringDictionaryColumnReader::next (ColumnReader.cc:561-594)
+      const uint64_t dict_size = c.dict_size;
+      const std::string cid = std::to_string(id);
+      if (dict_size > 0 && !has_len)
+        return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDictionaryColumn for column " + cid);
+      ORCG_ALLOC(int64_t, dlen, dict_size);
+      ORCG_ALLOC(int64_t, doff, dict_size + 1);
+      if ((rc = int_stream(c, kSlotLength, false, dict_size, dlen))) return rc;
+      if ((rc = launch_flag_negative(ctx, dlen, dict_size, d_scalars + 1))) return fail_ctx(rc);
+      if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
+      if ((rc = hip_check(ctx, hipMemcpyAsync(d_scalars, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream), "copy")))
+        return fail_ctx(rc);
+      uint64_t h[2] = {0, 0};  // blob bytes, negative-length flag
+      if ((rc = hip_check(ctx, hipMemcpyAsync(h, d_scalars, 16, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
+          (rc = sync_ctx(ctx)))
+        return fail_ctx(rc);
+      if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
+      StreamBuf& db = c.s[kSlotDict];
+      if (h[0] > 0 && !db.present)
+        return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
+      if (h[0] > (db.present ? db.len : 0)) return fail(ORCG_PARSE_ERROR, "bad read in readFully");
+      if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDictionaryColumn");
+      c.blob = db.present ? d_stage + db.host_off : nullptr;
+      c.blob_len = h[0];
+      ORCG_ALLOC(int64_t, idx, nonnull);
+      if ((rc = int_stream(c, kSlotData, false, nonnull, idx))) return rc;
+      int64_t* ridx = idx;
+      if (row_nn) {
+        ORCG_ALLOC_TO(int64_t, ridx, n);
+        if ((rc = scatter(idx, row_nn, n, ridx, 8))) return fail_ctx(rc);
+        if ((rc = hip_check(ctx, hipMemsetAsync(start, 0, n * 8, ctx->stream), "memset"))) return fail_ctx(rc);
+        if ((rc = hip_check(ctx, hipMemsetAsync(len, 0, n * 8, ctx->stream), "memset"))) return fail_ctx(rc);
+      }
+      if ((rc = launch_dict_gather(ctx, ridx, 8, row_nn, n, doff, dict_size, start, len))) return fail_ctx(rc);
+    } else {
+      if (!has_len) return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDirectColumn");
+      if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDirectColumn");
+      ORCG_ALLOC(int64_t, dlen, nonnull);
+      if ((rc = int_stream(c, kSlotLength, false, nonnull, dlen))) return rc;
+      ORCG_ALLOC(int64_t, dstart, nonnull + 1);
+      if ((rc = launch_exclusive_scan(ctx, dlen, nonnull, dstart))) return fail_ctx(rc);
+      StreamBuf& db = c.s[kSlotData];
+      c.blob = d_stage + db.host_off;
+      c.blob_len = db.len;
+      uint64_t need = 0;
+      if ((rc = hip_check(ctx, hipMemcpyAsync(&need, dstart + nonnull, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
+          (rc = sync_ctx(ctx)))
+        return fail_ctx(rc);
+      if (need > c.blob_len) return fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next");
+      if (row_nn) {
+        if ((rc = scatter(dstart, row_nn, n, start, 8))) return fail_ctx(rc);
+        if ((rc = scatter(dlen, row_nn, n, len, 8))) return fail_ctx(rc);
+      } else {
+        start = dstart;
+        len = dlen;
+      }
+    }
+    c.data = start;
+    c.length = len;
+  } else if (k == ORCG_TYPE_LIST || k == ORCG_TYPE_MAP) {
+    if (!has_len)
+      return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_LIST ? "LENGTH stream not found in List column"
+                                                        : "LENGTH stream not found in Map column");
+    ORCG_ALLOC(int64_t, dlen, nonnull);
+    if ((rc = int_stream(c, kSlotLength, false, nonnull, dlen))) return rc;
+    int64_t* rlen = dlen;
+    if (row_nn) {
+      ORCG_ALLOC_TO(int64_t, rlen, n);
+      if ((rc = scatter(dlen, row_nn, n, rlen, 8))) return fail_ctx(rc);
+    }
+    ORCG_ALLOC(int64_t, off, n + 1);
+    if ((rc = launch_exclusive_scan(ctx, rlen, n, off))) return fail_ctx(rc);
+    c.offsets = off;
+    uint64_t total = 0;
+    if ((rc = hip_check(ctx, hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
+        (rc = sync_ctx(ctx)))
+      return fail_ctx(rc);
+    for (uint32_t st : footer.types[id].subtypes)
+      if ((rc = decode(st, total, nullptr, total))) return rc;
+  } else if (k == ORCG_TYPE_STRUCT) {
+    for (uint32_t st : footer.types[id].subtypes)
+      if ((rc = decode(st, n, c.nn, nonnull))) return rc;
+  }
+  return ORCG_OK;
+}
+
+int orcg_reader::read_stripe(uint64_t s) {
+  if (!ctx) return fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
+  if (s >= footer.stripes.size()) return fail(ORCG_INVALID_ARGUMENT, "stripe index out of range");
+  hipSetDevice(ctx->device);
+  const double t0 = now_s();
+  const StripeInfo& si = footer.stripes[s];
+  std::string err;
+  // stripe footer (Reader.cc getStripeFooter :620-640)
+  std::vector<uint8_t> fb;
+  const uint64_t foff = si.offset + si.index_length + si.data_length;
+  if (foff + si.footer_length > file_len) return fail(ORCG_PARSE_ERROR, "stripe footer past the end of the file");
+  if (!read_range(file, foff, si.footer_length, ps.compression, ps.block_size, fb, err))
+    return fail(ORCG_PARSE_ERROR, err);
+  StripeFooter sf;
+  if (!parse_stripe_footer(fb.data(), fb.size(), si.offset, sf))
+    return fail(ORCG_PARSE_ERROR, std::string("bad StripeFooter from ") + compression_name(ps.compression));
+  // Reader.cc:634-640
+  if (sf.encodings.size() != cols.size())
+    return fail(ORCG_PARSE_ERROR, "bad number of ColumnEncodings in StripeFooter: expected=" +
+                                      std::to_string(cols.size()) + ", actual=" + std::to_string(sf.encodings.size()));
+  for (auto& c : cols) {
+    c.decoded = false;
+    c.has_nulls = false;
+    c.nn = nullptr;
+    c.data = nullptr;
+    c.length = c.offsets = nullptr;
+    c.blob = nullptr;
+    c.blob_len = 0;
+    for (auto& b : c.s) b = StreamBuf();
+  }
+  for (size_t i = 0; i < cols.size() && i < sf.encodings.size(); ++i) {
+    cols[i].encoding = sf.encodings[i].kind;
+    cols[i].dict_size = sf.encodings[i].dictionary_size;
+  }
+
+  // streams to read and their chunks
+  struct Need {
+    uint32_t col;
+    int slot;
+    std::vector<Chunk> chunks;
+  };
+  std::vector<Need> needs;
+  const uint64_t data_end = si.offset + si.index_length + si.data_length;
+  for (size_t i = 0; i < sf.streams.size(); ++i) {
+    const StreamInfo& st = sf.streams[i];
+    const int slot = slot_of(st.kind);
+    if (slot < 0 || st.column >= cols.size()) continue;
+    const Col& c = cols[st.column];
+    if (!c.selected || !is_supported(c.kind)) continue;
+    if (st.offset + st.length > data_end)
+      return fail(ORCG_PARSE_ERROR, "Malformed stream meta at stream index " + std::to_string(i) + " in stripe " +
+                                        std::to_string(s));
+    Need nd{st.column, slot, {}};
+    if (!split_chunks(file, st.offset, st.length, ps.compression, nd.chunks, err)) return fail(ORCG_PARSE_ERROR, err);
+    needs.push_back(std::move(nd));
+  }
+  // staging layout: every chunk gets a slot of its maximum size; compacted after
+  uint64_t at = 0;
+  std::vector<std::pair<size_t, size_t>> all;  // (need, chunk)
+  std::vector<uint64_t> stream_start(needs.size());
+  for (size_t i = 0; i < needs.size(); ++i) {
+    at = (at + 255) & ~(uint64_t)255;
+    stream_start[i] = at;
+    for (size_t j = 0; j < needs[i].chunks.size(); ++j) {
+      Chunk& ch = needs[i].chunks[j];
+      ch.dst_off = at;
+      at += ch.original ? ch.src_len : ps.block_size;
+      all.emplace_back(i, j);
+    }
+  }
+  const uint64_t slot_bytes = at;
+  // plans are appended after the compacted streams; reserve generously below
+  auto ensure_host = [&](uint64_t bytes) -> bool {
+    if (bytes <= h_cap) return true;
+    if (h_stage) (void)hipHostFree(h_stage);
+    h_stage = nullptr;
+    h_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(bytes + (bytes >> 2), 1 << 20);
+    if (hipHostMalloc((void**)&h_stage, cap, hipHostMallocDefault) != hipSuccess) return false;
+    h_cap = cap;
+    return true;
+  };
+  if (!ensure_host(slot_bytes + 64)) return fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
+  const double t1 = now_s();
+  std::vector<std::string> errs(all.size());
+  std::atomic<bool> bad{false};
+  parallel_for(all.size(), [&](size_t q) {
+    Chunk& ch = needs[all[q].first].chunks[all[q].second];
+    const uint64_t cap = ch.original ? ch.src_len : ps.block_size;
+    if (!decompress_chunk(ps.compression, file, ch, h_stage + ch.dst_off, cap, errs[q])) bad = true;
+  });
+  if (bad)
+    for (auto& e : errs)
+      if (!e.empty()) return fail(ORCG_PARSE_ERROR, e);
+  // compact each stream's chunks (destinations never pass their sources)
+  uint64_t w = 0;
+  for (size_t i = 0; i < needs.size(); ++i) {
+    w = (w + 255) & ~(uint64_t)255;
+    const uint64_t s0 = w;
+    for (auto& ch : needs[i].chunks) {
+      if (ch.dst_off != w) memmove(h_stage + w, h_stage + ch.dst_off, ch.dst_len);
+      w += ch.dst_len;
+    }
+    StreamBuf& sb = cols[needs[i].col].s[needs[i].slot];
+    sb.present = true;
+    sb.host_off = s0;
+    sb.len = w - s0;
+  }
+  (void)stream_start;
+  // host run plans (header walks only) for every RLE stream, in parallel
+  std::vector<StreamBuf*> rle;
+  std::vector<int> rle_kind;  // 0 byte RLE, 1 RLEv1, 2 RLEv2
+  for (auto& c : cols) {
+    if (!c.selected || !is_supported(c.kind)) continue;
+    const bool v1 = c.encoding == kDirect || c.encoding == kDictionary;
+    for (int sl = 0; sl < 3; ++sl) {
+      StreamBuf& sb = c.s[sl];
+      if (!sb.present) continue;
+      int kind;
+      if (sl == kSlotPresent) kind = 0;
+      else if (sl == kSlotData) {
+        if (c.kind == ORCG_TYPE_BOOLEAN || c.kind == ORCG_TYPE_BYTE) kind = 0;
+        else if (is_int_kind(c.kind) || (is_string_kind(c.kind) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)))
+          kind = v1 ? 1 : 2;
+        else continue;  // raw bytes
+      } else {
+        kind = v1 ? 1 : 2;
+      }
+      rle.push_back(&sb);
+      rle_kind.push_back(kind);
+    }
+  }
+  parallel_for(rle.size(), [&](size_t q) {
+    StreamBuf& sb = *rle[q];
+    const uint8_t* p = h_stage + sb.host_off;
+    if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, 16u << 10, 16384));
+    else if (rle_kind[q] == 1) sb.plan.reset(make_v1_plan(p, sb.len, 16u << 10, 8192));
+    else sb.plan.reset(make_plan(p, sb.len, 16u << 10, 8192));
+  });
+  uint64_t seg_bytes = 0;
+  for (auto* sb : rle) seg_bytes += ((sb->plan->segs.size() * sizeof(orcg_segment)) + 255) & ~(uint64_t)255;
+  w = (w + 255) & ~(uint64_t)255;
+  if (w + seg_bytes + 64 > h_cap) {
+    // grow, keeping the compacted streams
+    std::vector<uint8_t> keep(h_stage, h_stage + w);
+    if (!ensure_host(w + seg_bytes + 64)) return fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
+    memcpy(h_stage, keep.data(), w);
+  }
+  for (auto* sb : rle) {
+    sb->seg_off = w;
+    const size_t nb = sb->plan->segs.size() * sizeof(orcg_segment);
+    if (nb) memcpy(h_stage + w, sb->plan->segs.data(), nb);
+    w = (w + nb + 255) & ~(uint64_t)255;
+  }
+  const double t2 = now_s();
+
+  pool.release_all();
+  d_stage = (uint8_t*)pool.get(w + 64);
+  d_scalars = (uint64_t*)pool.get(64);
+  if (!d_stage || !d_scalars) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  int rc = hip_check(ctx, hipMemcpyAsync(d_stage, h_stage, w, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
+  if (rc) return fail_ctx(rc);
+  rc = sync_ctx(ctx);
+  if (rc) return fail_ctx(rc);
+  const double t3 = now_s();
+  rc = decode(0, si.num_rows, nullptr, si.num_rows);
+  if (!rc) {
+    rc = sync_ctx(ctx);
+    if (rc) rc = fail_ctx(rc);
+  }
+  const double t4 = now_s();
+  timings[0] = t1 - t0;
+  timings[1] = t2 - t1;
+  timings[2] = t3 - t2;
+  timings[3] = t4 - t3;
+  return rc;
+}
+
+static thread_local std::string t_open_error;
+
+extern "C" {
+
+const char* orcg_reader_open_error(void) { return t_open_error.c_str(); }
+
+int orcg_reader_open(orcg_ctx* ctx, const uint8_t* file, uint64_t file_len, orcg_reader** out) {
+  if (!out || (file_len && !file)) return ORCG_INVALID_ARGUMENT;
+  *out = nullptr;
+  std::unique_ptr<orcg_reader> r(new orcg_reader());
+  r->ctx = ctx;
+  r->file = file;
+  r->file_len = file_len;
+  const int rc = r->open_tail();
+  if (rc) {
+    t_open_error = r->last_error;
+    if (ctx) ctx->last_error = r->last_error;
+    return rc;
+  }
+  *out = r.release();
+  return ORCG_OK;
+}
+
+int orcg_reader_open_file(orcg_ctx* ctx, const char* path, orcg_reader** out) {
+  if (!out || !path) return ORCG_INVALID_ARGUMENT;
+  *out = nullptr;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) {
+    t_open_error = std::string("Can't open ") + path;
+    if (ctx) ctx->last_error = t_open_error;
+    return ORCG_INVALID_ARGUMENT;
+  }
+  struct stat st;
+  fstat(fd, &st);
+  const uint64_t len = (uint64_t)st.st_size;
+  void* m = len ? mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0) : nullptr;
+  close(fd);
+  if (len && m == MAP_FAILED) {
+    t_open_error = std::string("Can't map ") + path;
+    if (ctx) ctx->last_error = t_open_error;
+    return ORCG_INVALID_ARGUMENT;
+  }
+  std::unique_ptr<orcg_reader> r(new orcg_reader());
+  r->ctx = ctx;
+  r->file = (const uint8_t*)m;
+  r->file_len = len;
+  r->mapped = m;
+  const int rc = r->open_tail();
+  if (rc) {
+    t_open_error = r->last_error;
+    if (ctx) ctx->last_error = r->last_error;
+    return rc;
+  }
+  *out = r.release();
+  return ORCG_OK;
+}
+
+void orcg_reader_destroy(orcg_reader* r) { delete r; }
+const char* orcg_reader_last_error(const orcg_reader* r) { return r ? r->last_error.c_str() : "null reader"; }
+uint64_t orcg_reader_num_rows(const orcg_reader* r) { return r ? r->footer.num_rows : 0; }
+uint64_t orcg_reader_num_stripes(const orcg_reader* r) { return r ? r->footer.stripes.size() : 0; }
+uint32_t orcg_reader_row_index_stride(const orcg_reader* r) { return r ? r->footer.row_index_stride : 0; }
+uint32_t orcg_reader_compression(const orcg_reader* r) { return r ? r->ps.compression : 0; }
+uint64_t orcg_reader_compression_block_size(const orcg_reader* r) { return r ? r->ps.block_size : 0; }
+uint32_t orcg_reader_writer_version(const orcg_reader* r) { return r ? r->ps.writer_version : 0; }
+int orcg_reader_format_version(const orcg_reader* r, uint32_t* major, uint32_t* minor) {
+  if (!r || !major || !minor) return ORCG_INVALID_ARGUMENT;
+  // the reference reports 0.11 when the version is absent (FileVersion::v_0_11)
+  *major = r->ps.version.size() > 0 ? r->ps.version[0] : 0;
+  *minor = r->ps.version.size() > 1 ? r->ps.version[1] : 11;
+  return ORCG_OK;
+}
+uint32_t orcg_reader_num_types(const orcg_reader* r) { return r ? (uint32_t)r->footer.types.size() : 0; }
+int orcg_reader_type(const orcg_reader* r, uint32_t id, orcg_type_info* out) {
+  if (!r || !out || id >= r->footer.types.size()) return ORCG_INVALID_ARGUMENT;
+  const TypeInfo& t = r->footer.types[id];
+  out->kind = t.kind;
+  out->num_subtypes = (uint32_t)t.subtypes.size();
+  out->maximum_length = t.maximum_length;
+  out->precision = t.precision;
+  out->scale = t.scale;
+  return ORCG_OK;
+}
+int orcg_reader_subtypes(const orcg_reader* r, uint32_t id, uint32_t* out, uint32_t cap) {
+  if (!r || id >= r->footer.types.size() || (cap && !out)) return ORCG_INVALID_ARGUMENT;
+  const auto& st = r->footer.types[id].subtypes;
+  for (uint32_t i = 0; i < cap && i < st.size(); ++i) out[i] = st[i];
+  return ORCG_OK;
+}
+const char* orcg_reader_field_name(const orcg_reader* r, uint32_t id, uint32_t i) {
+  if (!r || id >= r->footer.types.size() || i >= r->footer.types[id].field_names.size()) return nullptr;
+  return r->footer.types[id].field_names[i].c_str();
+}
+int orcg_reader_stripe(const orcg_reader* r, uint64_t s, orcg_stripe_info* out) {
+  if (!r || !out || s >= r->footer.stripes.size()) return ORCG_INVALID_ARGUMENT;
+  const StripeInfo& si = r->footer.stripes[s];
+  out->offset = si.offset;
+  out->index_length = si.index_length;
+  out->data_length = si.data_length;
+  out->footer_length = si.footer_length;
+  out->num_rows = si.num_rows;
+  return ORCG_OK;
+}
+
+int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  const size_t nt = r->cols.size();
+  if (!include) {
+    for (auto& c : r->cols) c.selected = true;
+    return ORCG_OK;
+  }
+  if (ntypes > nt) return r->fail(ORCG_INVALID_ARGUMENT, "include list longer than the type list");
+  std::vector<uint32_t> parent(nt, 0);
+  for (size_t i = 0; i < nt; ++i)
+    for (uint32_t st : r->footer.types[i].subtypes) parent[st] = (uint32_t)i;
+  for (auto& c : r->cols) c.selected = false;
+  r->cols[0].selected = true;
+  for (uint32_t i = 0; i < ntypes; ++i) {
+    if (!include[i]) continue;
+    // the column, its subtree and its ancestors
+    for (uint32_t a = i; a != 0; a = parent[a]) r->cols[a].selected = true;
+    std::vector<uint32_t> st{i};
+    while (!st.empty()) {
+      const uint32_t x = st.back();
+      st.pop_back();
+      r->cols[x].selected = true;
+      for (uint32_t y : r->footer.types[x].subtypes) st.push_back(y);
+    }
+  }
+  return ORCG_OK;
+}
+
+int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  return r->read_stripe(stripe);
+}
+
+int orcg_reader_column(const orcg_reader* r, uint32_t id, orcg_column_view* out) {
+  if (!r || !out || id >= r->cols.size()) return ORCG_INVALID_ARGUMENT;
+  const Col& c = r->cols[id];
+  memset(out, 0, sizeof(*out));
+  out->type_id = id;
+  out->kind = c.kind;
+  out->encoding = c.encoding;
+  out->decoded = c.decoded ? 1u : 0u;
+  if (!c.decoded) return is_supported(c.kind) ? ORCG_OK : ORCG_INVALID_ARGUMENT;
+  out->num_elements = c.n;
+  out->has_nulls = c.has_nulls ? 1 : 0;
+  out->not_null = c.nn;
+  out->data = c.data;
+  out->length = c.length;
+  out->offsets = c.offsets;
+  out->blob = c.blob;
+  out->blob_len = c.blob_len;
+  return ORCG_OK;
+}
+
+int orcg_reader_copy_to_host(orcg_reader* r, void* dst, const void* src, uint64_t bytes) {
+  if (!r || !r->ctx || (bytes && (!dst || !src))) return ORCG_INVALID_ARGUMENT;
+  if (!bytes) return ORCG_OK;
+  int rc = hip_check(r->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, r->ctx->stream), "D2H");
+  if (!rc) rc = sync_ctx(r->ctx);
+  return rc;
+}
+
+int orcg_reader_last_timings(const orcg_reader* r, double* out4) {
+  if (!r || !out4) return ORCG_INVALID_ARGUMENT;
+  for (int i = 0; i < 4; ++i) out4[i] = r->timings[i];
+  return ORCG_OK;
+}
+
+}  // extern "C"

@@ -161,6 +161,21 @@ def rlev2_decode(data, n, is_signed, not_null=None, dtype=np.int64, ctx=None, ou
     return out
 
 
+def rlev1_decode(data, n, is_signed, not_null=None, dtype=np.int64, ctx=None, out=None):
+    """orcg_rlev1_decode_{i64,i32}: one-shot host-buffer RLEv1 decode
+    (RleDecoderV1::next, c++/src/RLEv1.cc:234-300)."""
+    L = _lib.load()
+    ctx = ctx or default_context()
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    if out is None:
+        out = np.zeros(n, dtype=dtype)
+    nn = None if not_null is None else np.ascontiguousarray(not_null, dtype=np.uint8)
+    fn = {8: L.orcg_rlev1_decode_i64, 4: L.orcg_rlev1_decode_i32}
+    check(fn[out.dtype.itemsize](ctx.handle, _ptr(buf), buf.size, int(bool(is_signed)), _ptr(nn), n,
+                                 _ptr(out)), ctx.last_error)
+    return out
+
+
 class Plan:
     """orcg_rlev2_plan: host run walk -> segments (+ first corrupt run)."""
 

@@ -13,13 +13,17 @@ from oracle import oracle
 from orc_amd import _lib
 import orc_amd
 
-HEADER = os.path.join(ROOT, "include", "orcg.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(orcg_\w+)\s*\(", text)))
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names |= set(re.findall(r"\b(orcg_\w+)\s*\(", text))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,0 +1,80 @@
+"""CPU tests of the file-level host logic (tail / footer parsing, schema,
+reference error texts) and of the parity checker itself: pyarrow's ORC
+reader against the reference's expected ColumnPrinter output
+(examples/expected/*.jsn.gz, tools/test/TestMatch.cc:124-151). No GPU."""
+import os
+
+import pytest
+
+import orc_amd
+from file_parity import (CORRUPT_FILES, PARITY_FILES, expected_json, path, printer_equal, pyarrow_rows,
+                         supported_fields, to_printer_form)
+
+
+def _pa():
+    return pytest.importorskip("pyarrow.orc")
+
+
+@pytest.mark.parametrize("name", PARITY_FILES)
+def test_tail_matches_pyarrow(name):
+    po = _pa()
+    r = orc_amd.Reader(path(name))  # metadata only: no device context
+    try:
+        f = po.ORCFile(path(name))
+    except Exception:
+        pytest.skip("pyarrow cannot open %s" % name)
+    assert r.num_rows == f.nrows
+    assert r.num_stripes == f.nstripes
+    if r.types[0].kind == 12:
+        assert r.types[0].field_names == [fld.name for fld in f.schema]
+    comp = {"UNCOMPRESSED": "NONE"}.get(f.compression, f.compression)
+    assert r.compression == comp
+    rows = sum(r.stripe(i)["num_rows"] for i in range(r.num_stripes))
+    assert rows == r.num_rows
+
+
+def test_tail_errors_use_reference_texts():
+    with pytest.raises(orc_amd.ParseError, match="File size too small"):
+        orc_amd.Reader(path("zero.orc"))
+    with pytest.raises(orc_amd.ParseError, match="Not an ORC file"):
+        orc_amd.Reader(b"XYZ" + bytes(100) + b"\x03")
+    with pytest.raises(orc_amd.InvalidArgument):
+        orc_amd.Reader(path("no_such_file.orc"))
+
+
+def test_stripe_read_needs_a_device_context():
+    r = orc_amd.Reader(path("TestOrcFile.test1.orc"))
+    with pytest.raises(orc_amd.InvalidArgument):
+        r.read_stripe(0)
+
+
+def test_type_strings():
+    r = orc_amd.Reader(path("TestOrcFile.test1.orc"))
+    assert r.type_string() == (
+        "struct<boolean1:boolean,byte1:tinyint,short1:smallint,int1:int,long1:bigint,float1:float,"
+        "double1:double,bytes1:binary,string1:string,middle:struct<list:array<struct<int1:int,string1:string>>>,"
+        "list:array<struct<int1:int,string1:string>>,map:map<string,struct<int1:int,string1:string>>>")
+    r = orc_amd.Reader(path("orc_index_int_string.orc"))
+    assert r.type_string() == "struct<_col0:int,_col1:varchar(4)>"
+
+
+@pytest.mark.parametrize("name", ["TestOrcFile.test1.orc", "nulls-at-end-snappy.orc", "orc_index_int_string.orc",
+                                  "TestStringDictionary.testRowIndex.orc"])
+def test_checker_pinned_to_reference_expected_output(name):
+    """pyarrow (the checker the GPU parity tests use) reproduces the
+    reference's own expected rows for these files."""
+    _pa()
+    want = expected_json(name)
+    assert want is not None
+    r = orc_amd.Reader(path(name))
+    fields = supported_fields(r)
+    got = [to_printer_form(row) for row in pyarrow_rows(name, fields)]
+    assert len(got) == len(want)
+    for i, (w, g) in enumerate(zip(want, got)):
+        w = {k: w[k] for k in fields}
+        assert printer_equal(w, g), "row %d: %r vs %r" % (i, w, g)
+
+
+def test_corrupt_fixtures_present():
+    for name, _ in CORRUPT_FILES:
+        assert os.path.exists(path(name))
