@@ -253,7 +253,59 @@ def main():
                     "batches": [None]})
     with open(os.path.join(HERE, "kat_boolrle.json"), "w") as f:
         json.dump(bool_fx, f, indent=1)
-    print("wrote %d rlev2, %d byte-rle, %d bool-rle fixtures" % (len(fx), len(byte_fx), len(bool_fx)))
+    # ------------------------------------------------------------------ RLEv1
+    v1_fx = []
+
+    def addv1(name, data, expected, signed, not_null=None, batches=None, seeks=None):
+        line, _ = blocks[("RLEv1", name)]
+        d = {"name": name, "source": "c++/test/TestRleDecoder.cc:%d" % line, "kind": "rlev1",
+             "signed": signed, "data": bytes(data).hex(), "expected": expected, "batches": batches or [None]}
+        if not_null is not None:
+            d["not_null"] = not_null
+        if seeks is not None:
+            d["seeks"] = seeks
+        v1_fx.append(d)
+
+    def v1body(name):
+        return blocks[("RLEv1", name)][1]
+
+    addv1("simpleTest", arrays(v1body("simpleTest"), "buffer")[0], [100 - i for i in range(100)] + [2, 3, 5, 7, 11],
+          False)
+    addv1("signedNullLiteralTest", arrays(v1body("signedNullLiteralTest"), "buffer")[0],
+          [i // 2 if i % 2 == 0 else -((i + 1) // 2) for i in range(8)], True, not_null=[1] * 8)
+    addv1("splitHeader", arrays(v1body("splitHeader"), "buffer")[0], [247864668] * 3, False)
+    addv1("splitRuns", arrays(v1body("splitRuns"), "buffer")[0], [255 + i for i in range(128)] + [1, 2, 3, 4, 5],
+          False, batches=[3])
+    addv1("testSigned", arrays(v1body("testSigned"), "buffer")[0], [16 - i for i in range(130)], True,
+          batches=[100, None])
+    # testNull: odd positions null, values count up through 10 batches of 24
+    exp, nn = [], []
+    for i in range(10):
+        for j in range(24):
+            on = (j + 1) % 2
+            nn.append(on)
+            exp.append(i * 24 + j if on else None)
+    addv1("testNull", arrays(v1body("testNull"), "buffer")[0], exp, True, not_null=nn, batches=[24])
+    addv1("testLeadingNulls", arrays(v1body("testLeadingNulls"), "buffer")[0], [None] * 5 + [1, 2, 3, 4, 5], False,
+          not_null=[0] * 5 + [1] * 5)
+    addv1("skipTest", arrays(v1body("skipTest"), "buffer")[0], [i if i < 1024 else 256 * i for i in range(2048)],
+          True, batches=[None, 7])
+    sb = v1body("seekTest")
+    junk = arrays(sb, "junk")[0]
+    file_loc = arrays(sb, "fileLoc")[0]
+    rle_loc = arrays(sb, "rleLoc")[0]
+    want = [i // 4 if i < 1024 else 2 * i for i in range(2048)] + junk
+
+    def at(i):
+        return want[i]
+
+    picks = list(range(0, 4096, 61)) + [1023, 1024, 2047, 2048, 4095]
+    addv1("seekTest", arrays(sb, "buffer")[0], want, True, batches=[2048],
+          seeks=[{"position": [file_loc[i], rle_loc[i]], "expected": [at(i)]} for i in picks])
+    with open(os.path.join(HERE, "kat_rlev1.json"), "w") as f:
+        json.dump(v1_fx, f, indent=1)
+    print("wrote %d rlev2, %d byte-rle, %d bool-rle, %d rlev1 fixtures" % (len(fx), len(byte_fx), len(bool_fx),
+                                                                         len(v1_fx)))
 
 
 if __name__ == "__main__":

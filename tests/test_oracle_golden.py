@@ -13,6 +13,7 @@ from oracle import oracle
 RLEV2 = load_golden("kat_rlev2.json")
 BYTE = load_golden("kat_byterle.json")
 BOOL = load_golden("kat_boolrle.json")
+RLEV1 = load_golden("kat_rlev1.json")
 
 
 def _batches(fx):
@@ -71,6 +72,20 @@ def test_boolrle_kat(fx):
         dec = oracle.ByteRleDecoder(data, boolean=True)
         got = decode_batches(dec.next, fx["expected"], b, nn)
         assert_matches(fx["expected"], got, nn, fx["name"])
+
+
+@pytest.mark.parametrize("fx", RLEV1, ids=[f["name"] for f in RLEV1])
+def test_rlev1_kat(fx):
+    data = bytes.fromhex(fx["data"])
+    nn = fx.get("not_null")
+    for b in _batches(fx):
+        dec = oracle.RleDecoderV1(data, fx["signed"])
+        got = decode_batches(dec.next, fx["expected"], b, nn)
+        assert_matches(fx["expected"], got, nn, "%s batch=%s" % (fx["name"], b))
+    for sk in fx.get("seeks", []):
+        dec = oracle.RleDecoderV1(data, fx["signed"])
+        dec.seek(*sk["position"])
+        assert list(dec.next(len(sk["expected"]))) == sk["expected"]
 
 
 def test_rlev2_errors_match_reference_messages():
