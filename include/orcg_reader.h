@@ -111,13 +111,20 @@ int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes);
  * reader (valid until the next read or destroy). Synchronous. */
 int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe);
 int orcg_reader_column(const orcg_reader* r, uint32_t type_id, orcg_column_view* out);
+/* Stripes [first, first + count) into HBM, all kept resident: the host
+ * decompresses and plans stripe i + 1 on a worker thread while the GPU
+ * decodes stripe i. orcg_reader_stripe_column(r, k, ...) views the k-th. */
+int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count);
+int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t type_id, orcg_column_view* out);
 
 /* Device -> host copy on the reader's context stream (synchronous). */
 int orcg_reader_copy_to_host(orcg_reader* r, void* host_dst, const void* device_src, uint64_t bytes);
 
-/* Host time split of the last orcg_reader_read_stripe, in seconds:
- * [0] tail/footer + chunk split, [1] decompression, [2] H2D, [3] decode (device). */
-int orcg_reader_last_timings(const orcg_reader* r, double* out4);
+/* Time split of the last read, in seconds, summed over its stripes:
+ * [0] stripe footer + chunk split, [1] decompression, [2] run plans (host
+ * threads), [3] H2D, [4] device decode. With read_stripes, [0..2] of
+ * stripe i + 1 overlap [3..4] of stripe i. */
+int orcg_reader_last_timings(const orcg_reader* r, double* out5);
 
 #ifdef __cplusplus
 }

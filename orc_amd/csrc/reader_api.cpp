@@ -117,7 +117,7 @@ struct StreamBuf {
 };
 
 struct Col {
-  bool selected = true, decoded = false;
+  bool decoded = false;
   uint32_t kind = 0, encoding = 0;
   uint64_t n = 0;
   bool has_nulls = false;
@@ -145,6 +145,62 @@ int slot_of(uint32_t stream_kind) {
 
 }  // namespace
 
+// One stripe prepared on the host: stream bytes decompressed into pinned
+// staging, run plans and their segment tables appended (no device work).
+struct HostStage {
+  uint64_t stripe = ~0ull;
+  std::vector<Col> cols;  // streams (and, while decoding, the outputs)
+  uint8_t* h = nullptr;   // pinned staging
+  size_t cap = 0;
+  uint64_t used = 0;
+  int rc = ORCG_OK;
+  std::string err;
+  double t_parse = 0, t_decomp = 0, t_plan = 0;
+  ~HostStage() {
+    if (h) (void)hipHostFree(h);
+  }
+  bool ensure(uint64_t bytes, uint64_t keep) {
+    if (bytes <= cap) return true;
+    const uint64_t ncap = std::max<uint64_t>(bytes + (bytes >> 2), 1 << 20);
+    uint8_t* nh = nullptr;
+    if (hipHostMalloc((void**)&nh, ncap, hipHostMallocDefault) != hipSuccess) return false;
+    if (h) {
+      if (keep) memcpy(nh, h, keep);
+      (void)hipHostFree(h);
+    }
+    h = nh;
+    cap = ncap;
+    return true;
+  }
+  int fail(int status, const std::string& m) {
+    rc = status;
+    err = m;
+    return status;
+  }
+};
+
+struct ColOut {
+  bool decoded = false;
+  uint32_t kind = 0, encoding = 0;
+  uint64_t n = 0;
+  bool has_nulls = false;
+  const uint8_t* nn = nullptr;
+  const void* data = nullptr;
+  const int64_t* length = nullptr;
+  const int64_t* offsets = nullptr;
+  const uint8_t* blob = nullptr;
+  uint64_t blob_len = 0;
+};
+
+// One decoded stripe in HBM: its device allocations and column views.
+struct DevSlot {
+  uint64_t stripe = ~0ull;
+  DevPool pool;
+  uint8_t* d_stage = nullptr;
+  uint64_t* d_scalars = nullptr;
+  std::vector<ColOut> out;
+};
+
 struct orcg_reader {
   Ctx* ctx = nullptr;
   const uint8_t* file = nullptr;
@@ -152,17 +208,18 @@ struct orcg_reader {
   void* mapped = nullptr;
   PostScript ps;
   Footer footer;
-  std::vector<Col> cols;
+  std::vector<uint8_t> selected;  // per type id
   std::string last_error;
-  DevPool pool;
-  uint8_t* h_stage = nullptr;  // pinned staging
-  size_t h_cap = 0;
-  uint8_t* d_stage = nullptr;  // device copy of the staging buffer
-  uint64_t* d_scalars = nullptr;
-  double timings[4] = {0, 0, 0, 0};
+  HostStage stages[2];
+  std::vector<std::unique_ptr<DevSlot>> slots;  // results of the last read, in stripe order
+  size_t nslots = 0;
+  // decode() state: the host stage and device slot of the stripe being decoded
+  HostStage* H = nullptr;
+  DevSlot* D = nullptr;
+  double timings[5] = {0, 0, 0, 0, 0};
 
   ~orcg_reader() {
-    if (h_stage) (void)hipHostFree(h_stage);
+    slots.clear();
     if (mapped) munmap(mapped, file_len);
   }
   int fail(int status, const std::string& m) {
@@ -173,7 +230,9 @@ struct orcg_reader {
   int fail_ctx(int rc) { return fail(rc, ctx ? ctx->last_error : std::string("device error")); }
 
   int open_tail();
-  int read_stripe(uint64_t s);
+  int prepare(uint64_t s, HostStage& hs) const;
+  int read_stripes(uint64_t first, uint64_t count);
+  int upload_and_decode(HostStage& hs, DevSlot& ds);
   int decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count);
   int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out);
   int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out);
@@ -181,7 +240,7 @@ struct orcg_reader {
   int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
   template <typename T>
   T* alloc(uint64_t count) {
-    return (T*)pool.get(std::max<uint64_t>(count, 1) * sizeof(T));
+    return (T*)D->pool.get(std::max<uint64_t>(count, 1) * sizeof(T));
   }
 };
 
@@ -229,14 +288,13 @@ int orcg_reader::open_tail() {
                                           std::to_string(j) + ") in types(" + std::to_string(i) + ")");
     }
   }
-  cols = std::vector<Col>(nt);
-  for (size_t i = 0; i < nt; ++i) cols[i].kind = footer.types[i].kind;
+  selected.assign(nt, 1);
   return ORCG_OK;
 }
 
 int orcg_reader::nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out) {
-  int rc = launch_count_nonzero(ctx, nn, n, d_scalars);
-  if (!rc) rc = hip_check(ctx, hipMemcpyAsync(&out, d_scalars, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H count");
+  int rc = launch_count_nonzero(ctx, nn, n, D->d_scalars);
+  if (!rc) rc = hip_check(ctx, hipMemcpyAsync(&out, D->d_scalars, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H count");
   if (!rc) rc = sync_ctx(ctx);
   return rc;
 }
@@ -254,8 +312,8 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
     const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)(v1 ? kErrV1BadRead : kErrBadRead);
     return fail(dev_error_status(e), dev_error_message(e));
   }
-  const uint8_t* d_src = d_stage + sb.host_off;
-  const uint64_t* d_seg = (const uint64_t*)(d_stage + sb.seg_off);
+  const uint8_t* d_src = D->d_stage + sb.host_off;
+  const uint64_t* d_seg = (const uint64_t*)(D->d_stage + sb.seg_off);
   const int sg = is_signed ? 1 : 0;
   int rc;
   if (c.encoding == kDirect || c.encoding == kDictionary)
@@ -274,7 +332,7 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
     const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)kErrByteBadRead;
     return fail(dev_error_status(e), dev_error_message(e));
   }
-  const int rc = launch_byterle(ctx, d_stage + sb.host_off, sb.len, (const uint64_t*)(d_stage + sb.seg_off),
+  const int rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, (const uint64_t*)(D->d_stage + sb.seg_off),
                                 sb.plan->segs.size(), boolean, 0, count, out);
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
@@ -287,8 +345,8 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   if (!v) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed")
 
 int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count) {
-  Col& c = cols[id];
-  if (!c.selected || !is_supported(c.kind)) return ORCG_OK;
+  Col& c = H->cols[id];
+  if (!selected[id] || !is_supported(c.kind)) return ORCG_OK;
   c.n = n;
   c.decoded = true;
   int rc;
@@ -341,7 +399,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     StreamBuf& sb = c.s[kSlotData];
     const uint64_t w = k == ORCG_TYPE_FLOAT ? 4 : 8;
     if (sb.len < w * nonnull) return fail(ORCG_PARSE_ERROR, "bad read in DoubleColumnReader::next()");
-    const void* raw = d_stage + sb.host_off;
+    const void* raw = D->d_stage + sb.host_off;
     double* dense;
     if (k == ORCG_TYPE_FLOAT) {
       ORCG_ALLOC_TO(double, dense, nonnull);
@@ -370,12 +428,12 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       ORCG_ALLOC(int64_t, dlen, dict_size);
       ORCG_ALLOC(int64_t, doff, dict_size + 1);
       if ((rc = int_stream(c, kSlotLength, false, dict_size, dlen))) return rc;
-      if ((rc = launch_flag_negative(ctx, dlen, dict_size, d_scalars + 1))) return fail_ctx(rc);
+      if ((rc = launch_flag_negative(ctx, dlen, dict_size, D->d_scalars + 1))) return fail_ctx(rc);
       if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
-      if ((rc = hip_check(ctx, hipMemcpyAsync(d_scalars, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream), "copy")))
+      if ((rc = hip_check(ctx, hipMemcpyAsync(D->d_scalars, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream), "copy")))
         return fail_ctx(rc);
       uint64_t h[2] = {0, 0};  // blob bytes, negative-length flag
-      if ((rc = hip_check(ctx, hipMemcpyAsync(h, d_scalars, 16, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
+      if ((rc = hip_check(ctx, hipMemcpyAsync(h, D->d_scalars, 16, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
           (rc = sync_ctx(ctx)))
         return fail_ctx(rc);
       if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
@@ -384,7 +442,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
         return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
       if (h[0] > (db.present ? db.len : 0)) return fail(ORCG_PARSE_ERROR, "bad read in readFully");
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDictionaryColumn");
-      c.blob = db.present ? d_stage + db.host_off : nullptr;
+      c.blob = db.present ? D->d_stage + db.host_off : nullptr;
       c.blob_len = h[0];
       ORCG_ALLOC(int64_t, idx, nonnull);
       if ((rc = int_stream(c, kSlotData, false, nonnull, idx))) return rc;
@@ -404,7 +462,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       ORCG_ALLOC(int64_t, dstart, nonnull + 1);
       if ((rc = launch_exclusive_scan(ctx, dlen, nonnull, dstart))) return fail_ctx(rc);
       StreamBuf& db = c.s[kSlotData];
-      c.blob = d_stage + db.host_off;
+      c.blob = D->d_stage + db.host_off;
       c.blob_len = db.len;
       uint64_t need = 0;
       if ((rc = hip_check(ctx, hipMemcpyAsync(&need, dstart + nonnull, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
@@ -448,42 +506,36 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   return ORCG_OK;
 }
 
-int orcg_reader::read_stripe(uint64_t s) {
-  if (!ctx) return fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
-  if (s >= footer.stripes.size()) return fail(ORCG_INVALID_ARGUMENT, "stripe index out of range");
-  hipSetDevice(ctx->device);
+// Host half of a stripe read (thread-safe w.r.t. the device half of another
+// stripe): stripe footer (Reader.cc getStripeFooter :620-640), stream
+// location (StripeStream.cc:82-125), decompression of every selected stream
+// (Compression.cc) in parallel chunks, run plans + segment tables.
+int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
+  hs.stripe = s;
+  hs.rc = ORCG_OK;
+  hs.err.clear();
   const double t0 = now_s();
   const StripeInfo& si = footer.stripes[s];
   std::string err;
-  // stripe footer (Reader.cc getStripeFooter :620-640)
   std::vector<uint8_t> fb;
   const uint64_t foff = si.offset + si.index_length + si.data_length;
-  if (foff + si.footer_length > file_len) return fail(ORCG_PARSE_ERROR, "stripe footer past the end of the file");
+  if (foff + si.footer_length > file_len) return hs.fail(ORCG_PARSE_ERROR, "stripe footer past the end of the file");
   if (!read_range(file, foff, si.footer_length, ps.compression, ps.block_size, fb, err))
-    return fail(ORCG_PARSE_ERROR, err);
+    return hs.fail(ORCG_PARSE_ERROR, err);
   StripeFooter sf;
   if (!parse_stripe_footer(fb.data(), fb.size(), si.offset, sf))
-    return fail(ORCG_PARSE_ERROR, std::string("bad StripeFooter from ") + compression_name(ps.compression));
+    return hs.fail(ORCG_PARSE_ERROR, std::string("bad StripeFooter from ") + compression_name(ps.compression));
   // Reader.cc:634-640
-  if (sf.encodings.size() != cols.size())
-    return fail(ORCG_PARSE_ERROR, "bad number of ColumnEncodings in StripeFooter: expected=" +
-                                      std::to_string(cols.size()) + ", actual=" + std::to_string(sf.encodings.size()));
-  for (auto& c : cols) {
-    c.decoded = false;
-    c.has_nulls = false;
-    c.nn = nullptr;
-    c.data = nullptr;
-    c.length = c.offsets = nullptr;
-    c.blob = nullptr;
-    c.blob_len = 0;
-    for (auto& b : c.s) b = StreamBuf();
+  const size_t nt = footer.types.size();
+  if (sf.encodings.size() != nt)
+    return hs.fail(ORCG_PARSE_ERROR, "bad number of ColumnEncodings in StripeFooter: expected=" +
+                                         std::to_string(nt) + ", actual=" + std::to_string(sf.encodings.size()));
+  hs.cols = std::vector<Col>(nt);
+  for (size_t i = 0; i < nt; ++i) {
+    hs.cols[i].kind = footer.types[i].kind;
+    hs.cols[i].encoding = sf.encodings[i].kind;
+    hs.cols[i].dict_size = sf.encodings[i].dictionary_size;
   }
-  for (size_t i = 0; i < cols.size() && i < sf.encodings.size(); ++i) {
-    cols[i].encoding = sf.encodings[i].kind;
-    cols[i].dict_size = sf.encodings[i].dictionary_size;
-  }
-
-  // streams to read and their chunks
   struct Need {
     uint32_t col;
     int slot;
@@ -494,23 +546,20 @@ int orcg_reader::read_stripe(uint64_t s) {
   for (size_t i = 0; i < sf.streams.size(); ++i) {
     const StreamInfo& st = sf.streams[i];
     const int slot = slot_of(st.kind);
-    if (slot < 0 || st.column >= cols.size()) continue;
-    const Col& c = cols[st.column];
-    if (!c.selected || !is_supported(c.kind)) continue;
+    if (slot < 0 || st.column >= nt) continue;
+    if (!selected[st.column] || !is_supported(hs.cols[st.column].kind)) continue;
     if (st.offset + st.length > data_end)
-      return fail(ORCG_PARSE_ERROR, "Malformed stream meta at stream index " + std::to_string(i) + " in stripe " +
-                                        std::to_string(s));
+      return hs.fail(ORCG_PARSE_ERROR, "Malformed stream meta at stream index " + std::to_string(i) + " in stripe " +
+                                           std::to_string(s));
     Need nd{st.column, slot, {}};
-    if (!split_chunks(file, st.offset, st.length, ps.compression, nd.chunks, err)) return fail(ORCG_PARSE_ERROR, err);
+    if (!split_chunks(file, st.offset, st.length, ps.compression, nd.chunks, err)) return hs.fail(ORCG_PARSE_ERROR, err);
     needs.push_back(std::move(nd));
   }
-  // staging layout: every chunk gets a slot of its maximum size; compacted after
+  // staging: every chunk gets a slot of its maximum size, compacted after
   uint64_t at = 0;
-  std::vector<std::pair<size_t, size_t>> all;  // (need, chunk)
-  std::vector<uint64_t> stream_start(needs.size());
+  std::vector<std::pair<size_t, size_t>> all;
   for (size_t i = 0; i < needs.size(); ++i) {
     at = (at + 255) & ~(uint64_t)255;
-    stream_start[i] = at;
     for (size_t j = 0; j < needs[i].chunks.size(); ++j) {
       Chunk& ch = needs[i].chunks[j];
       ch.dst_off = at;
@@ -518,50 +567,38 @@ int orcg_reader::read_stripe(uint64_t s) {
       all.emplace_back(i, j);
     }
   }
-  const uint64_t slot_bytes = at;
-  // plans are appended after the compacted streams; reserve generously below
-  auto ensure_host = [&](uint64_t bytes) -> bool {
-    if (bytes <= h_cap) return true;
-    if (h_stage) (void)hipHostFree(h_stage);
-    h_stage = nullptr;
-    h_cap = 0;
-    const uint64_t cap = std::max<uint64_t>(bytes + (bytes >> 2), 1 << 20);
-    if (hipHostMalloc((void**)&h_stage, cap, hipHostMallocDefault) != hipSuccess) return false;
-    h_cap = cap;
-    return true;
-  };
-  if (!ensure_host(slot_bytes + 64)) return fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
+  if (!hs.ensure(at + 64, 0)) return hs.fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
   const double t1 = now_s();
   std::vector<std::string> errs(all.size());
   std::atomic<bool> bad{false};
   parallel_for(all.size(), [&](size_t q) {
     Chunk& ch = needs[all[q].first].chunks[all[q].second];
     const uint64_t cap = ch.original ? ch.src_len : ps.block_size;
-    if (!decompress_chunk(ps.compression, file, ch, h_stage + ch.dst_off, cap, errs[q])) bad = true;
+    if (!decompress_chunk(ps.compression, file, ch, hs.h + ch.dst_off, cap, errs[q])) bad = true;
   });
   if (bad)
     for (auto& e : errs)
-      if (!e.empty()) return fail(ORCG_PARSE_ERROR, e);
-  // compact each stream's chunks (destinations never pass their sources)
-  uint64_t w = 0;
+      if (!e.empty()) return hs.fail(ORCG_PARSE_ERROR, e);
+  uint64_t w = 0;  // compact (destinations never pass their sources)
   for (size_t i = 0; i < needs.size(); ++i) {
     w = (w + 255) & ~(uint64_t)255;
     const uint64_t s0 = w;
     for (auto& ch : needs[i].chunks) {
-      if (ch.dst_off != w) memmove(h_stage + w, h_stage + ch.dst_off, ch.dst_len);
+      if (ch.dst_off != w) memmove(hs.h + w, hs.h + ch.dst_off, ch.dst_len);
       w += ch.dst_len;
     }
-    StreamBuf& sb = cols[needs[i].col].s[needs[i].slot];
+    StreamBuf& sb = hs.cols[needs[i].col].s[needs[i].slot];
     sb.present = true;
     sb.host_off = s0;
     sb.len = w - s0;
   }
-  (void)stream_start;
+  const double t15 = now_s();
   // host run plans (header walks only) for every RLE stream, in parallel
   std::vector<StreamBuf*> rle;
   std::vector<int> rle_kind;  // 0 byte RLE, 1 RLEv1, 2 RLEv2
-  for (auto& c : cols) {
-    if (!c.selected || !is_supported(c.kind)) continue;
+  for (size_t i = 0; i < nt; ++i) {
+    Col& c = hs.cols[i];
+    if (!selected[i] || !is_supported(c.kind)) continue;
     const bool v1 = c.encoding == kDirect || c.encoding == kDictionary;
     for (int sl = 0; sl < 3; ++sl) {
       StreamBuf& sb = c.s[sl];
@@ -570,7 +607,8 @@ int orcg_reader::read_stripe(uint64_t s) {
       if (sl == kSlotPresent) kind = 0;
       else if (sl == kSlotData) {
         if (c.kind == ORCG_TYPE_BOOLEAN || c.kind == ORCG_TYPE_BYTE) kind = 0;
-        else if (is_int_kind(c.kind) || (is_string_kind(c.kind) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)))
+        else if (is_int_kind(c.kind) ||
+                 (is_string_kind(c.kind) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)))
           kind = v1 ? 1 : 2;
         else continue;  // raw bytes
       } else {
@@ -582,7 +620,7 @@ int orcg_reader::read_stripe(uint64_t s) {
   }
   parallel_for(rle.size(), [&](size_t q) {
     StreamBuf& sb = *rle[q];
-    const uint8_t* p = h_stage + sb.host_off;
+    const uint8_t* p = hs.h + sb.host_off;
     if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, 16u << 10, 16384));
     else if (rle_kind[q] == 1) sb.plan.reset(make_v1_plan(p, sb.len, 16u << 10, 8192));
     else sb.plan.reset(make_plan(p, sb.len, 16u << 10, 8192));
@@ -590,40 +628,97 @@ int orcg_reader::read_stripe(uint64_t s) {
   uint64_t seg_bytes = 0;
   for (auto* sb : rle) seg_bytes += ((sb->plan->segs.size() * sizeof(orcg_segment)) + 255) & ~(uint64_t)255;
   w = (w + 255) & ~(uint64_t)255;
-  if (w + seg_bytes + 64 > h_cap) {
-    // grow, keeping the compacted streams
-    std::vector<uint8_t> keep(h_stage, h_stage + w);
-    if (!ensure_host(w + seg_bytes + 64)) return fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
-    memcpy(h_stage, keep.data(), w);
-  }
+  if (!hs.ensure(w + seg_bytes + 64, w)) return hs.fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
   for (auto* sb : rle) {
     sb->seg_off = w;
     const size_t nb = sb->plan->segs.size() * sizeof(orcg_segment);
-    if (nb) memcpy(h_stage + w, sb->plan->segs.data(), nb);
+    if (nb) memcpy(hs.h + w, sb->plan->segs.data(), nb);
     w = (w + nb + 255) & ~(uint64_t)255;
   }
+  hs.used = w;
   const double t2 = now_s();
+  hs.t_parse = t1 - t0;
+  hs.t_decomp = t15 - t1;
+  hs.t_plan = t2 - t15;
+  return ORCG_OK;
+}
 
-  pool.release_all();
-  d_stage = (uint8_t*)pool.get(w + 64);
-  d_scalars = (uint64_t*)pool.get(64);
-  if (!d_stage || !d_scalars) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
-  int rc = hip_check(ctx, hipMemcpyAsync(d_stage, h_stage, w, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
+// Device half: one H2D of the staging buffer, then every selected column.
+int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
+  const double t0 = now_s();
+  ds.stripe = hs.stripe;
+  ds.pool.release_all();
+  ds.d_stage = (uint8_t*)ds.pool.get(hs.used + 64);
+  ds.d_scalars = (uint64_t*)ds.pool.get(64);
+  if (!ds.d_stage || !ds.d_scalars) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  int rc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, hs.used, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
+  if (!rc) rc = sync_ctx(ctx);
   if (rc) return fail_ctx(rc);
-  rc = sync_ctx(ctx);
-  if (rc) return fail_ctx(rc);
-  const double t3 = now_s();
-  rc = decode(0, si.num_rows, nullptr, si.num_rows);
+  const double t1 = now_s();
+  H = &hs;
+  D = &ds;
+  rc = decode(0, footer.stripes[hs.stripe].num_rows, nullptr, footer.stripes[hs.stripe].num_rows);
   if (!rc) {
     rc = sync_ctx(ctx);
     if (rc) rc = fail_ctx(rc);
   }
-  const double t4 = now_s();
-  timings[0] = t1 - t0;
-  timings[1] = t2 - t1;
-  timings[2] = t3 - t2;
-  timings[3] = t4 - t3;
+  ds.out.assign(hs.cols.size(), ColOut());
+  for (size_t i = 0; i < hs.cols.size(); ++i) {
+    const Col& c = hs.cols[i];
+    ColOut& o = ds.out[i];
+    o.kind = c.kind;
+    o.encoding = c.encoding;
+    o.decoded = c.decoded && !rc;
+    o.n = c.n;
+    o.has_nulls = c.has_nulls;
+    o.nn = c.nn;
+    o.data = c.data;
+    o.length = c.length;
+    o.offsets = c.offsets;
+    o.blob = c.blob;
+    o.blob_len = c.blob_len;
+  }
+  H = nullptr;
+  D = nullptr;
+  timings[3] += t1 - t0;
+  timings[4] += now_s() - t1;
   return rc;
+}
+
+// Stripes [first, first + count): the host prepares stripe i + 1 on a
+// worker thread while the GPU decodes stripe i.
+int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
+  if (!ctx) return fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
+  if (first > footer.stripes.size() || count > footer.stripes.size() - first)
+    return fail(ORCG_INVALID_ARGUMENT, "stripe index out of range");
+  hipSetDevice(ctx->device);
+  for (auto& t : timings) t = 0;
+  while (slots.size() < count) slots.emplace_back(new DevSlot());
+  nslots = 0;
+  if (count == 0) return ORCG_OK;
+  int rc = prepare(first, stages[0]);
+  timings[0] += stages[0].t_parse;
+  timings[1] += stages[0].t_decomp;
+  timings[2] += stages[0].t_plan;
+  if (rc) return fail(rc, stages[0].err);
+  for (uint64_t k = 0; k < count; ++k) {
+    HostStage& cur = stages[k & 1];
+    HostStage& nxt = stages[(k + 1) & 1];
+    std::thread worker;
+    const bool more = k + 1 < count;
+    if (more) worker = std::thread([&, k] { prepare(first + k + 1, nxt); });
+    rc = upload_and_decode(cur, *slots[k]);
+    if (more) worker.join();
+    if (rc) return rc;
+    nslots = k + 1;
+    if (more) {
+      timings[0] += nxt.t_parse;
+      timings[1] += nxt.t_decomp;
+      timings[2] += nxt.t_plan;
+      if (nxt.rc) return fail(nxt.rc, nxt.err);
+    }
+  }
+  return ORCG_OK;
 }
 
 static thread_local std::string t_open_error;
@@ -732,26 +827,26 @@ int orcg_reader_stripe(const orcg_reader* r, uint64_t s, orcg_stripe_info* out) 
 
 int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes) {
   if (!r) return ORCG_INVALID_ARGUMENT;
-  const size_t nt = r->cols.size();
+  const size_t nt = r->selected.size();
   if (!include) {
-    for (auto& c : r->cols) c.selected = true;
+    for (auto& c : r->selected) c = 1;
     return ORCG_OK;
   }
   if (ntypes > nt) return r->fail(ORCG_INVALID_ARGUMENT, "include list longer than the type list");
   std::vector<uint32_t> parent(nt, 0);
   for (size_t i = 0; i < nt; ++i)
     for (uint32_t st : r->footer.types[i].subtypes) parent[st] = (uint32_t)i;
-  for (auto& c : r->cols) c.selected = false;
-  r->cols[0].selected = true;
+  for (auto& c : r->selected) c = 0;
+  r->selected[0] = 1;
   for (uint32_t i = 0; i < ntypes; ++i) {
     if (!include[i]) continue;
     // the column, its subtree and its ancestors
-    for (uint32_t a = i; a != 0; a = parent[a]) r->cols[a].selected = true;
+    for (uint32_t a = i; a != 0; a = parent[a]) r->selected[a] = 1;
     std::vector<uint32_t> st{i};
     while (!st.empty()) {
       const uint32_t x = st.back();
       st.pop_back();
-      r->cols[x].selected = true;
+      r->selected[x] = 1;
       for (uint32_t y : r->footer.types[x].subtypes) st.push_back(y);
     }
   }
@@ -760,18 +855,23 @@ int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes) 
 
 int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe) {
   if (!r) return ORCG_INVALID_ARGUMENT;
-  return r->read_stripe(stripe);
+  return r->read_stripes(stripe, 1);
 }
 
-int orcg_reader_column(const orcg_reader* r, uint32_t id, orcg_column_view* out) {
-  if (!r || !out || id >= r->cols.size()) return ORCG_INVALID_ARGUMENT;
-  const Col& c = r->cols[id];
+int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  return r->read_stripes(first, count);
+}
+
+int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t id, orcg_column_view* out) {
+  if (!r || !out || id >= r->footer.types.size() || k >= r->nslots) return ORCG_INVALID_ARGUMENT;
+  const ColOut& c = r->slots[k]->out[id];
   memset(out, 0, sizeof(*out));
   out->type_id = id;
-  out->kind = c.kind;
+  out->kind = r->footer.types[id].kind;
   out->encoding = c.encoding;
   out->decoded = c.decoded ? 1u : 0u;
-  if (!c.decoded) return is_supported(c.kind) ? ORCG_OK : ORCG_INVALID_ARGUMENT;
+  if (!c.decoded) return is_supported(out->kind) ? ORCG_OK : ORCG_INVALID_ARGUMENT;
   out->num_elements = c.n;
   out->has_nulls = c.has_nulls ? 1 : 0;
   out->not_null = c.nn;
@@ -783,6 +883,10 @@ int orcg_reader_column(const orcg_reader* r, uint32_t id, orcg_column_view* out)
   return ORCG_OK;
 }
 
+int orcg_reader_column(const orcg_reader* r, uint32_t id, orcg_column_view* out) {
+  return orcg_reader_stripe_column(r, 0, id, out);
+}
+
 int orcg_reader_copy_to_host(orcg_reader* r, void* dst, const void* src, uint64_t bytes) {
   if (!r || !r->ctx || (bytes && (!dst || !src))) return ORCG_INVALID_ARGUMENT;
   if (!bytes) return ORCG_OK;
@@ -791,9 +895,9 @@ int orcg_reader_copy_to_host(orcg_reader* r, void* dst, const void* src, uint64_
   return rc;
 }
 
-int orcg_reader_last_timings(const orcg_reader* r, double* out4) {
-  if (!r || !out4) return ORCG_INVALID_ARGUMENT;
-  for (int i = 0; i < 4; ++i) out4[i] = r->timings[i];
+int orcg_reader_last_timings(const orcg_reader* r, double* out5) {
+  if (!r || !out5) return ORCG_INVALID_ARGUMENT;
+  for (int i = 0; i < 5; ++i) out5[i] = r->timings[i];
   return ORCG_OK;
 }
 

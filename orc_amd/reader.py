@@ -231,9 +231,24 @@ class Reader:
             raise _lib.InvalidArgument("reader was opened without a device context")
         check(self._L.orcg_reader_read_stripe(self._h, i), self._err)
 
+    def read_stripes_device(self, first=0, count=None):
+        """Decode stripes [first, first + count) into HBM with the host
+        decompressing stripe i + 1 while the GPU decodes stripe i; every
+        stripe's batches stay resident (stripe_column_view)."""
+        if self._ctx is None:
+            raise _lib.InvalidArgument("reader was opened without a device context")
+        if count is None:
+            count = self.num_stripes - first
+        check(self._L.orcg_reader_read_stripes(self._h, first, count), self._err)
+
     def column_view(self, tid):
         v = _lib.ColumnView()
         check(self._L.orcg_reader_column(self._h, tid, ctypes.byref(v)), self._err)
+        return v
+
+    def stripe_column_view(self, k, tid):
+        v = _lib.ColumnView()
+        check(self._L.orcg_reader_stripe_column(self._h, k, tid, ctypes.byref(v)), self._err)
         return v
 
     def read_stripe(self, i):
@@ -263,9 +278,10 @@ class Reader:
         return Batch(self, cols)
 
     def last_timings(self):
-        t = (ctypes.c_double * 4)()
+        t = (ctypes.c_double * 5)()
         check(self._L.orcg_reader_last_timings(self._h, t))
-        return {"host_parse_s": t[0], "host_decompress_plan_s": t[1], "h2d_s": t[2], "device_decode_s": t[3]}
+        return {"host_parse_s": t[0], "host_decompress_s": t[1], "host_plan_s": t[2], "h2d_s": t[3],
+                "device_decode_s": t[4]}
 
     def read(self, fields=None):
         """All rows as dicts of the root struct's fields (pyarrow to_pylist shape)."""
