@@ -87,8 +87,8 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--stride", type=int, default=10_000)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -131,24 +131,29 @@ def main():
     def step():
         orc_amd.decode_positions_device(ctx, d_src, d_pos, args.stride, N, True, d_out)
 
-    for _ in range(args.warmup):
-        step()
-    ctx.synchronize()
+    # verify one decode first, then warm up: the host-side compare leaves the
+    # GPU idle for ~1 s, and the timed steps must not start from idle clocks
     if not args.no_verify:
+        step()
+        ctx.synchronize()
         ok = torch.equal(d_out.cpu(), torch.from_numpy(values))
         if not ok:
             raise SystemExit("decode mismatch on rank %d" % rank)
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    # one event between consecutive launches on the decode stream: per-launch
+    # durations with no gaps inserted between kernels
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    evs[0].record(stream)
     for i in range(args.steps):
-        starts[i].record(stream)
         step()
-        ends[i].record(stream)
+        evs[i + 1].record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -159,7 +164,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    kern_ms = float(np.mean([evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]))
 
     copy_incl = None
     if args.copy_inclusive and rank == 0:

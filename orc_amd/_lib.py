@@ -8,7 +8,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liborcgpu.so")
+# ORCG_LIB selects another in-tree build (e.g. liborcgpu_prof.so, the
+# phase-profiling variant used by scripts/phase_prof.py)
+LIB_PATH = os.path.join(HERE, os.environ.get("ORCG_LIB", "liborcgpu.so"))
 
 ORCG_OK = 0
 ORCG_PARSE_ERROR = 1

@@ -6,8 +6,11 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-OUT = os.path.join(HERE, "liborcgpu.so")
-OBJ = os.path.join(HERE, "build")
+# ORCG_PHASE_PROF=1 builds the phase-profiling variant (kernel cycle counters,
+# scripts/phase_prof.py) as liborcgpu_prof.so next to the product library.
+PROF = os.environ.get("ORCG_PHASE_PROF", "") == "1"
+OUT = os.path.join(HERE, "liborcgpu_prof.so" if PROF else "liborcgpu.so")
+OBJ = os.path.join(HERE, "build_prof" if PROF else "build")
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "encoder.cpp"]
@@ -16,6 +19,8 @@ HEADERS = ["orcg_internal.hh", "rlev2_device.hh", "orc_file.hh", os.path.join(".
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value"]
+if PROF:
+    FLAGS.append("-DORCG_PHASE_PROF")
 
 
 def _mtime(p):
@@ -41,7 +46,7 @@ def build(force=False, verbose=False):
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
     if force or _mtime(OUT) < max(_mtime(o) for o in objs):
-        cmd = [HIPCC, "-shared", "-fPIC", "-o", OUT] + objs + ["-Wl,-soname,liborcgpu.so", "-lz", "-ldl", "-lpthread"]
+        cmd = [HIPCC, "-shared", "-fPIC", "-o", OUT] + objs + ["-Wl,-soname," + os.path.basename(OUT), "-lz", "-ldl", "-lpthread"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

@@ -36,6 +36,15 @@ __device__ __forceinline__ uint32_t closest_fixed_bits(uint32_t n) {
 // unZigZag (c++/src/RLE.hh:32-34)
 __device__ __forceinline__ uint64_t unzigzag(uint64_t v) { return (v >> 1) ^ (0 - (v & 1)); }
 
+// Values the wave agrees on but the compiler cannot prove uniform (loaded
+// from LDS or computed from such loads): readfirstlane puts them in SGPRs, so
+// the code that depends on them stays scalar (a v_readlane with a VGPR lane
+// index becomes a waterfall loop).
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x);
+}
+
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
 }

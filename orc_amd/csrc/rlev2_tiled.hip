@@ -27,10 +27,51 @@ namespace orcg {
 namespace {
 using namespace dev;
 
+// Phase profiling (build with -DORCG_PHASE_PROF, scripts/phase_prof.py):
+// thread 0 adds the cycles between consecutive phase marks to g_phase[k].
+#ifdef ORCG_PHASE_PROF
+__device__ unsigned long long g_phase[16];
+#define PROF_MARK(k)                                                        \
+  do {                                                                      \
+    if (threadIdx.x == 0) {                                                 \
+      const uint64_t now_ = wall_clock64();                                 \
+      atomicAdd(&g_phase[k], (unsigned long long)(now_ - prof_last_));      \
+      prof_last_ = now_;                                                    \
+    }                                                                       \
+  } while (0)
+#define PROF_DECL uint64_t prof_last_ = wall_clock64()
+#else
+#define PROF_MARK(k) \
+  do {               \
+  } while (0)
+#define PROF_DECL
+#endif
+
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
 constexpr uint32_t kMaxRun = 4608;  // >= 4356, the longest legal run
-constexpr int kMaxRuns = 512;       // run-table capacity per window
+
+// Dense (short-run) mode. A stream of short runs (SHORT_REPEAT-heavy
+// low-cardinality columns: 2-9 bytes per run) makes the one-wave serial header
+// walk the bottleneck. Dense mode discovers run starts in parallel over a slab
+// of kSlab bytes: thread t owns bytes [t*kBlk, (t+1)*kBlk) and computes, for
+// every position of its block, the chain exit "first run start past the block
+// if a run started here" and the values in between (a backward scan, since a
+// run ending inside the block continues from a later position of the same
+// block); one lane then chains the 256 blocks (one LDS read per block instead
+// of one header parse per run), and every thread re-walks its own block from
+// its true entry to emit the run table. Short runs are then expanded one lane
+// per run into a per-wave LDS stage, flushed with coalesced stores.
+constexpr uint32_t kSlab = 2048;
+constexpr uint32_t kBlk = kSlab / kThreads;  // 8 bytes per thread
+constexpr uint32_t kDenseRuns = kSlab / 2;   // every run is >= 2 bytes
+constexpr uint32_t kStage = 256;             // values staged per wave
+constexpr uint32_t kShortL = 16;             // runs of <= kShortL values go lane-per-run
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr uint32_t kDpErr = 0x80000000u;     // DP entry: a corrupt run starts here
+constexpr uint16_t kSink = 0xffffu;          // chain successor: none
+// density hysteresis (stream bytes per run of the last pass)
+constexpr uint32_t kToDense = 24, kToSerial = 64;
 
 // kOpt bits
 constexpr int kOptNTStore = 1;  // non-temporal output stores (streamed, never re-read)
@@ -274,16 +315,17 @@ struct WalkResult {
 // Wave-uniform header walk over the window [wpos, wpos + kWin): records runs
 // starting at pos.. into (run_off, run_val) until the next run starts past
 // kWin - kMaxRun, leaves the segment, or the table is full.
-template <uint32_t kWin>
+template <uint32_t kWin, uint32_t kCap>
 __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_off, uint32_t* run_val,
                                            uint64_t wpos, uint64_t pos, uint64_t vi, uint64_t seg_end,
                                            uint64_t src_len, uint64_t value_end, int is_signed,
-                                           unsigned long long* err, int lane, uint32_t lim = kWin) {
+                                           unsigned long long* err, int lane, uint32_t lim = kWin,
+                                           uint32_t cap = kCap) {
   constexpr uint32_t kChunk = kWin - kMaxRun;
   uint64_t p = pos, v = vi;
   uint32_t n = 0, stop = 0;
   LaneWin hw;
-  while (p < seg_end && v < value_end && n < (uint32_t)kMaxRuns) {
+  while (p < seg_end && v < value_end && n < cap) {
     const uint32_t lp = (uint32_t)(p - wpos);
     if (lp >= kChunk && n > 0) break;  // starts in the next window
     hw.cover(win, lp, kWin / 4 + 8, lane);
@@ -307,22 +349,345 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
   return WalkResult{n, stop, (uint32_t)(p - pos), (uint32_t)(v - vi)};
 }
 
+// ---- dense mode -----------------------------------------------------------
+
+struct DenseResult {
+  uint32_t n, stop, dpos, dval;
+};
+
+// Header of the run at window offset lq, with every check the serial walk
+// applies (same order): truncated stream, run past the segment, run past the
+// loaded bytes. Returns the error code (kErrNone when the run is good).
+__device__ __forceinline__ uint32_t checked_run(const uint32_t* win, uint32_t lq, uint64_t wpos, uint64_t seg_end,
+                                                uint64_t src_len, uint32_t need, int is_signed, Run* out) {
+  const uint64_t pabs = wpos + lq;
+  const uint64_t avail = pabs < src_len ? src_len - pabs : 0;
+  const Run r = parse_run([&](uint32_t i) { return lds_byte(win, lq + i); }, avail, kHdrLim, is_signed);
+  uint32_t e = r.err;
+  if (e == kErrNone && pabs + r.bytes > seg_end) e = kErrBadSegment;
+  if (e == kErrNone && lq + r.bytes > need) e = kErrBadRead;
+  *out = r;
+  return e;
+}
+
+// Discover the runs that start in [sb, sb + lim) of the window (sb = the
+// window offset of `pos`, a run start) into s_off/s_val, with the serial
+// walk's stop rules (segment end, value end, first corrupt run). All threads.
+__device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint32_t* s_dp, uint32_t* s_off,
+                                                      uint32_t* s_val, uint16_t* s_nxt, uint8_t* s_mark,
+                                                      uint32_t* s_ctl, uint64_t wpos, uint32_t sb, uint32_t lim,
+                                                      uint64_t vi, uint64_t seg_end, uint64_t src_len,
+                                                      uint64_t value_end, uint32_t need, int is_signed,
+                                                      unsigned long long* err, int tid
+#ifdef ORCG_PHASE_PROF
+                                                      , uint64_t& prof_last_
+#endif
+) {
+  const int wave = tid / kWave, lane = tid % kWave;
+  const uint32_t lo = (uint32_t)tid * kBlk, hi = lo + kBlk;
+  // discovery is a chain of barriers: keep its issue priority above the
+  // expanding waves of co-resident workgroups
+  __builtin_amdgcn_s_setprio(2);
+  // (1) backward scan over the block: s_dp[q] = exit | values << 15, or
+  // kDpErr where the extent parse cannot vouch for the run (corrupt header,
+  // run past the stream / segment / loaded bytes, over-long varints); a
+  // kDpErr on the chain only hands the rest of the slab to the exact walk.
+  {
+    // the block's bytes and 32 more, byte-aligned to the block (sb is
+    // wave-uniform, so is the shift)
+    const uint32_t a0 = sb + lo, sh = a0 & 3u, w0 = a0 >> 2;
+    uint32_t raw[kBlk / 4 + 9], b4[kBlk / 4 + 8];
+#pragma unroll
+    for (int i = 0; i < (int)kBlk / 4 + 9; ++i) raw[i] = win[w0 + i];
+#pragma unroll
+    for (int i = 0; i < (int)kBlk / 4 + 8; ++i) b4[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
+    // terminator mask: bit i = byte i < 0x80 (bytes kBlk .. kBlk + 31 too)
+    uint64_t term = 0;
+#pragma unroll
+    for (int i = 0; i < (int)kBlk / 4 + 8 && i < 16; ++i) {
+      const uint32_t m = (~b4[i] >> 7) & 0x01010101u;
+      term |= (uint64_t)((m * 0x10204080u) >> 28) << (4 * i);
+    }
+    auto B = [&](int i) -> uint32_t { return (b4[i >> 2] >> ((i & 3) * 8)) & 0xffu; };
+#pragma unroll
+    for (int e = (int)kBlk - 1; e >= 0; --e) {
+      const uint32_t q = lo + (uint32_t)e;
+      const uint32_t fb = B(e), b1 = B(e + 1), b2 = B(e + 2), b3 = B(e + 3);
+      const uint32_t kind = fb >> 6;
+      const uint32_t W = fbs_width((fb >> 1) & 0x1fu);
+      const uint32_t L2 = ((fb & 1u) << 8 | b1) + 1u;
+      uint32_t bytes, L;
+      bool ok = true;
+      if (kind == 0) {
+        bytes = 2u + ((fb >> 3) & 7u);
+        L = (fb & 7u) + 3u;
+      } else if (kind == 1) {
+        bytes = 2u + (W * L2 + 7u) / 8u;
+        L = L2;
+      } else if (kind == 2) {
+        const uint32_t bw = (b2 >> 5) + 1u, pbs = fbs_width(b2 & 0x1fu), pgw = (b3 >> 5) + 1u, pl = b3 & 0x1fu;
+        ok = pl != 0 && pbs + pgw <= 64;
+        bytes = 4u + bw + (W * L2 + 7u) / 8u + (closest_fixed_bits(pbs + pgw) * pl + 7u) / 8u;
+        L = L2;
+      } else {
+        const uint32_t Wd = ((fb >> 1) & 0x1fu) ? W : 0u;
+        const uint64_t t1 = term >> (e + 2);
+        const uint32_t n1 = t1 ? (uint32_t)__builtin_ctzll(t1) + 1u : 64u;  // first varint's bytes
+        const uint64_t t2 = n1 < 32 ? t1 >> n1 : 0;
+        const uint32_t n2 = t2 ? (uint32_t)__builtin_ctzll(t2) + 1u : 64u;
+        ok = n1 <= 12 && n2 <= 12 && !(Wd != 0 && L2 < 2);
+        bytes = 2u + n1 + n2 + (Wd ? (Wd * (L2 - 2u) + 7u) / 8u : 0u);
+        L = L2;
+      }
+      const uint32_t lq = sb + q;
+      const uint64_t pabs = wpos + lq;
+      ok = ok && pabs + bytes <= src_len && pabs + bytes <= seg_end && lq + bytes <= need;
+      uint32_t ent;
+      if (!ok) {
+        ent = kDpErr;
+      } else {
+        const uint32_t nx = q + bytes;
+        if (nx >= hi) {
+          ent = nx | (L << 15);
+        } else {
+          const uint32_t t = s_dp[nx];
+          ent = (t & kDpErr) ? kDpErr : t + (L << 15);
+        }
+      }
+      s_dp[q] = ent;
+    }
+  }
+  __syncthreads();
+  PROF_MARK(3);
+  // (2) the chain from position 0 by pointer doubling. N(q) = the first run
+  // start past q's block if a run starts at q (kSink: corrupt / past the
+  // slab). Level i marks N^(2^i) of every marked position and squares N, so
+  // after 8 levels the first 256 chain elements (one per block at most) are
+  // marked. Marks only grow and every marked position is a chain element, so
+  // reading a mark another thread sets in the same level is harmless.
+  {
+    uint16_t* na = s_nxt;
+    uint16_t* nb = s_nxt + kSlab;
+#pragma unroll
+    for (uint32_t e = 0; e < kBlk; ++e) {
+      const uint32_t q = lo + e, t = s_dp[q], x = t & 0x7fffu;
+      na[q] = ((t & kDpErr) || x >= lim) ? kSink : (uint16_t)x;
+      s_mark[q] = q == 0;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int lev = 0; lev < 8; ++lev) {
+#pragma unroll
+      for (uint32_t e = 0; e < kBlk; ++e) {
+        const uint32_t q = lo + e, n = na[q];
+        if (n != kSink) {
+          if (s_mark[q]) s_mark[n] = 1;
+          nb[q] = na[n];
+        } else {
+          nb[q] = kSink;
+        }
+      }
+      __syncthreads();
+      uint16_t* t = na;
+      na = nb;
+      nb = t;
+    }
+  }
+  PROF_MARK(4);
+  // (3) block b's entry = its marked position; values before it = exclusive
+  // scan of the entries' value counts. Every thread walks its block from its
+  // entry with the exact checks: count, then emit.
+  uint32_t eb = kNone;
+#pragma unroll
+  for (uint32_t e = kBlk; e-- > 0;)
+    if (s_mark[lo + e]) eb = lo + e;
+  const uint32_t cb = (eb != kNone && !(s_dp[eb] & kDpErr)) ? s_dp[eb] >> 15 : 0u;
+  uint32_t* s_wsum = s_ctl + 4;
+  const uint32_t cincl = wave_scan_u32(cb);
+  if (lane == kWave - 1) s_wsum[wave] = cincl;
+  if (tid == 0) {
+    s_ctl[8] = kNone;  // first block whose walk stopped inside it
+    s_ctl[9] = 0;      // last block with an entry
+    s_ctl[3] = 0;      // stop (corrupt run)
+  }
+  __syncthreads();
+  uint32_t vb = cincl - cb;
+  for (int w = 0; w < wave; ++w) vb += s_wsum[w];
+  __syncthreads();  // s_wsum is reused by the run-count scan
+  uint32_t cnt = 0, p = eb, v = vb;
+  if (eb != kNone) {
+    while (p < hi && p < lim && wpos + sb + p < seg_end && vi + v < value_end) {
+      Run r;
+      const uint32_t e = checked_run(win, sb + p, wpos, seg_end, src_len, need, is_signed, &r);
+      if (e != kErrNone) {
+        report(err, vi + v, e);
+        s_ctl[3] = 1;
+        break;
+      }
+      ++cnt;
+      p += r.bytes;
+      v += r.L;
+    }
+    if (p < hi) atomicMin(&s_ctl[8], (uint32_t)tid);
+    atomicMax(&s_ctl[9], (uint32_t)tid);
+  }
+  // block-wide exclusive scan of the counts
+  const uint32_t incl = wave_scan_u32(cnt);
+  if (lane == kWave - 1) s_wsum[wave] = incl;
+  __syncthreads();
+  uint32_t base = incl - cnt;
+  for (int w = 0; w < wave; ++w) base += s_wsum[w];
+  const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  {
+    // the pass ends where the first early-stopping block stopped, else at
+    // the exit of the last block with an entry
+    const uint32_t fin = s_ctl[8] != kNone ? s_ctl[8] : s_ctl[9];
+    if ((uint32_t)tid == fin) {
+      s_ctl[1] = p;
+      s_ctl[2] = v;
+    }
+  }
+  // the DP table is dead: the run table may overwrite it (s_dp aliases
+  // s_off/s_val), but only once every thread has walked
+  __syncthreads();
+  if (cnt) {
+    p = eb;
+    v = vb;
+    for (uint32_t k = 0; k < cnt; ++k) {
+      Run r;
+      checked_run(win, sb + p, wpos, seg_end, src_len, need, is_signed, &r);
+      s_off[base + k] = sb + p;
+      s_val[base + k] = v;
+      p += r.bytes;
+      v += r.L;
+    }
+  }
+  __syncthreads();
+  PROF_MARK(5);
+  __builtin_amdgcn_s_setprio(0);
+  return DenseResult{uni(total), uni(s_ctl[3]), uni(s_ctl[1]), uni(s_ctl[2])};
+}
+
+// Value j of a short run (kind SHORT_REPEAT / DIRECT / DELTA) parsed at
+// window offset `hoff`; `acc` carries a variable-width DELTA run's |delta| sum.
+__device__ __forceinline__ uint64_t short_value(const uint32_t* win, const Run& r, uint32_t hoff, uint32_t j,
+                                                int is_signed, uint64_t& acc) {
+  if (r.kind == 0) return r.a;
+  if (r.kind == 1) {
+    const uint32_t bit = j * r.W;
+    const uint32_t br = hoff + r.data + (bit >> 3);
+    uint64_t v = field(lds12(win, br), br, bit & 7u, r.W);
+    return is_signed ? unzigzag(v) : v;
+  }
+  if (r.W == 0) return r.a + (uint64_t)j * r.b;
+  if (j == 0) return r.a;
+  const uint64_t v1 = r.a + r.b;
+  if (j == 1) return v1;
+  const uint32_t bit = (j - 2) * r.W;
+  const uint32_t br = hoff + r.data + (bit >> 3);
+  acc += field(lds12(win, br), br, bit & 7u, r.W);
+  return (int64_t)r.b < 0 ? v1 - acc : v1 + acc;
+}
+
+// Expand runs [r0, r1) of the run table with one wave: maximal groups of
+// consecutive short runs (<= kStage values) are decoded one lane per run into
+// the wave's LDS stage and flushed with coalesced stores; any other run
+// (long, PATCHED_BASE) goes through expand_run.
+template <int kOpt, typename T>
+__device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nwords, const uint32_t* s_off,
+                                             const uint32_t* s_val, uint64_t* stage, uint32_t r0, uint32_t r1,
+                                             uint64_t vi, int is_signed, uint64_t value_begin, uint64_t value_end,
+                                             T* dst, int lane) {
+  uint32_t c = r0;
+  while (c < r1) {
+    const uint32_t r = c + (uint32_t)lane;
+    const bool act = r < r1;
+    const uint32_t hoff = act ? s_off[r] : s_off[c];
+    const uint32_t val = act ? s_val[r] : 0u;
+    const Run run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
+    const bool shortr = act && run.kind != 2 && run.L <= kShortL;
+    const uint32_t Ls = shortr ? run.L : 0u;
+    const uint32_t incl = wave_scan_u32(Ls);
+    const uint64_t bad = __ballot(!(shortr && incl <= kStage));
+    const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : (uint32_t)kWave;
+    if (k == 0) {
+      expand_run<kOpt>(win, nwords, uni(s_off[c]), vi + uni(s_val[c]), is_signed, value_begin, value_end, dst, lane);
+      ++c;
+      continue;
+    }
+    const bool mine = (uint32_t)lane < k;
+    const uint32_t st0 = incl - Ls;
+    uint32_t maxl = mine ? Ls : 0u;
+    for (int m = 32; m >= 1; m >>= 1) maxl = max(maxl, (uint32_t)__shfl_xor((int)maxl, m));
+    uint64_t acc = 0;
+    for (uint32_t j = 0; j < maxl; ++j)
+      if (mine && j < Ls) stage[st0 + j] = short_value(win, run, hoff, j, is_signed, acc);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t tot = rdlane(incl, k - 1);
+    const uint64_t g0 = vi + rdlane(val, 0);
+    for (uint32_t o = (uint32_t)lane; o < tot; o += kWave) {
+      const uint64_t g = g0 + o;
+      if (g >= value_begin && g < value_end) store1<kOpt>(dst + (g - value_begin), stage[o]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    c += k;
+  }
+}
+
 __device__ __forceinline__ void lds_barrier() {
   // LDS ordering only: never drains the output stores (vmcnt).
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMinWaves>
+// Dense-mode LDS (only instantiated when kDense): block entries and the
+// per-wave value stages.
+template <bool kDense>
+struct DenseLds {
+  union {
+    uint64_t stage[kThreads / kWave][kStage];  // expansion: per-wave value stages
+    uint16_t nxt[2][kSlab];                    // discovery: chain successors (double-buffered)
+  };
+  uint8_t mark[kSlab];                         // discovery: chain marks
+};
+template <>
+struct DenseLds<false> {};
+
+template <bool kDense>
+__device__ __forceinline__ uint16_t* s_dense_nxt(DenseLds<kDense>& d) {
+  if constexpr (kDense) return &d.nxt[0][0];
+  else return nullptr;
+}
+template <bool kDense>
+__device__ __forceinline__ uint8_t* s_dense_mark(DenseLds<kDense>& d) {
+  if constexpr (kDense) return d.mark;
+  else return nullptr;
+}
+
+template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMinWaves, bool kDense = false>
 __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint8_t* __restrict__ src, uint64_t src_len, int is_signed,
     const uint64_t* __restrict__ segtab, uint64_t nsegs, uint64_t rows_per_group,
     uint64_t value_begin, uint64_t nvalues, T* __restrict__ dst, unsigned long long* err) {
   constexpr uint32_t kWin = kWinKB * 1024u;
+  constexpr uint32_t kChunk = kWin - kMaxRun;
   constexpr int kBufs = kPipe ? 2 : 1;
+  static_assert(!(kDense && kPipe), "dense mode is a non-pipelined instance");
+  // run table capacity; in dense instances the slab DP table aliases it
+  constexpr uint32_t kCap = kDense ? kDenseRuns : 512u;
+  static_assert(!kDense || 2 * kCap >= kSlab, "DP table must fit the run table");
+  static_assert(!kDense || kChunk >= kSlab, "window too small for a slab");
   __shared__ uint32_t s_win[kBufs][kWin / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
-  __shared__ uint32_t s_off[kBufs][kMaxRuns];
-  __shared__ uint32_t s_val[kBufs][kMaxRuns];
-  __shared__ uint32_t s_ctl[kBufs][4];
+  __shared__ uint32_t s_tab[kBufs][2 * kCap];
+  __shared__ uint32_t s_ctl[kBufs][12];
+  __shared__ DenseLds<kDense> s_dense;
+  uint32_t* s_off[kBufs];
+  uint32_t* s_val[kBufs];
+  for (int b = 0; b < kBufs; ++b) {
+    s_off[b] = s_tab[b];
+    s_val[b] = s_tab[b] + kCap;
+  }
 
   const uint64_t g = blockIdx.x;
   const int tid = (int)threadIdx.x;
@@ -354,9 +719,12 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   const uint64_t bias = (uint64_t)(base_abs - (uintptr_t)src);  // stream offset of descriptor byte 0
 
   uint64_t pos = seg_start;
+  PROF_DECL;
   if constexpr (!kPipe) {
     uint64_t pwpos = ~0ull;  // previous window (stream offset) and its valid bytes
     uint32_t pneed = 0;
+    bool dense = false;      // wave-uniform mode of the next pass (dense instances only)
+    bool probe = true;       // the segment's first pass
     while (pos < seg_end && vi < value_end) {
       const uint32_t wrel = (uint32_t)(pos - bias) & ~15u;
       const uint64_t wpos = bias + wrel;
@@ -367,10 +735,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         if (end_rel - wrel < need) need = (uint32_t)(end_rel - wrel);
         // the previous window's tail [wpos, pwpos + pneed) is already in LDS:
         // move it to the front instead of re-reading it (source and
-        // destination must not overlap: the shift is at least the length)
-        // A walk that stopped on a full run table (many tiny runs) may have
-        // advanced less than the tail it would keep: then reload instead of
-        // an overlapping LDS move.
+        // destination must not overlap: the shift is at least the length;
+        // otherwise reload)
         if (pwpos != ~0ull && pwpos + pneed > wpos && wpos - pwpos >= pwpos + pneed - wpos) {
           keep = (uint32_t)(pwpos + pneed - wpos);
           if (keep > need) keep = need;
@@ -390,25 +756,77 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (wave == 0) {
-        const WalkResult w = walk<kWin>(s_win[0], s_off[0], s_val[0], wpos, pos, vi, seg_end, src_len,
-                                        value_end, is_signed, err, lane, need);
-        if (lane == 0) {
-          s_ctl[0][0] = w.n;
-          s_ctl[0][1] = w.stop;
-          s_ctl[0][2] = w.dpos;
-          s_ctl[0][3] = w.dval;
+      PROF_MARK(0);
+      // every run that starts in the window's first kChunk bytes ends inside
+      // it: consume them all (several passes) before moving the window
+      do {
+        uint32_t n, stop, dpos, dval;
+        bool was_dense = false;
+        if constexpr (kDense) was_dense = dense;
+        if (was_dense) {
+          const uint32_t sb = (uint32_t)(pos - wpos);
+          const uint32_t lim = min(kSlab, kChunk - sb);
+          const DenseResult d =
+              dense_discover(s_win[0], s_tab[0], s_off[0], s_val[0], s_dense_nxt(s_dense), s_dense_mark(s_dense),
+                             s_ctl[0], wpos, sb, lim, vi, seg_end, src_len, value_end, need, is_signed, err, tid
+#ifdef ORCG_PHASE_PROF
+                             , prof_last_
+#endif
+              );
+          n = d.n;
+          stop = d.stop;
+          dpos = d.dpos;
+          dval = d.dval;
+          if constexpr (kDense) {
+            const uint32_t r0 = (uint32_t)(((uint64_t)n * wave) / kWaves), r1 = (uint32_t)(((uint64_t)n * (wave + 1)) / kWaves);
+            dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], s_dense.stage[wave], r0, r1, vi, is_signed,
+                               value_begin, value_end, dst, lane);
+          }
+        } else {
+          if (wave == 0) {
+            // the walk is the workgroup's critical path (the other waves wait
+            // at the barrier): raise its issue priority over co-resident
+            // waves that are expanding
+            __builtin_amdgcn_s_setprio(3);
+            // dense instances: a short first walk (the probe) measures the
+            // stream's bytes per run before committing to a mode
+            const uint32_t cap = (kDense && probe) ? 32u : kCap;
+            const WalkResult w = walk<kWin, kCap>(s_win[0], s_off[0], s_val[0], wpos, pos, vi, seg_end, src_len,
+                                                  value_end, is_signed, err, lane, need, cap);
+            if (lane == 0) {
+              s_ctl[0][0] = w.n;
+              s_ctl[0][1] = w.stop;
+              s_ctl[0][2] = w.dpos;
+              s_ctl[0][3] = w.dval;
+            }
+            __builtin_amdgcn_s_setprio(0);
+          }
+          __syncthreads();
+          PROF_MARK(1);
+          n = uni(s_ctl[0][0]);
+          stop = uni(s_ctl[0][1]);
+          dpos = uni(s_ctl[0][2]);
+          dval = uni(s_ctl[0][3]);
+          for (uint32_t k = wave; k < n; k += kWaves)
+            expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][k]), vi + uni(s_val[0][k]), is_signed,
+                             value_begin, value_end, dst, lane);
         }
-      }
-      __syncthreads();
-      const uint32_t n = s_ctl[0][0], stop = s_ctl[0][1];
-      const uint64_t next_pos = pos + s_ctl[0][2], next_vi = vi + s_ctl[0][3];
-      for (uint32_t k = wave; k < n; k += kWaves)
-        expand_run<kOpt>(s_win[0], kWin / 4 + 8, s_off[0][k], vi + s_val[0][k], is_signed, value_begin, value_end, dst, lane);
-      __syncthreads();  // the window is refilled next
-      if (stop) return;
-      pos = next_pos;
-      vi = next_vi;
+        __syncthreads();  // the run table (and the window) are rewritten next
+        PROF_MARK(was_dense ? 6 : 2);
+        if (stop) return;
+        pos += dpos;
+        vi += dval;
+        probe = false;
+        if constexpr (kDense) {
+          // hysteresis on the stream bytes per run of this pass
+          if (n > 0) {
+            const uint32_t bpr = dpos / n;
+            if (!dense && n >= 8 && bpr < kToDense) dense = true;
+            else if (dense && bpr >= kToSerial) dense = false;
+          }
+        }
+        if (n == 0 && dpos == 0) break;  // nothing consumed (cannot happen for a good window)
+      } while (pos < wpos + kChunk && pos < seg_end && vi < value_end);
       pwpos = wpos;
       pneed = need;
     }
@@ -418,7 +836,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       const uint32_t wrel = (uint32_t)(pos - bias) & ~15u;
       fill<kOpt>(s_win[0], rs, wrel, kWin, 0, 1, lane);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const WalkResult w = walk<kWin>(s_win[0], s_off[0], s_val[0], bias + wrel, pos, vi, seg_end, src_len,
+      const WalkResult w = walk<kWin, kCap>(s_win[0], s_off[0], s_val[0], bias + wrel, pos, vi, seg_end, src_len,
                                       value_end, is_signed, err, lane);
       if (lane == 0) {
         s_ctl[0][0] = w.n;
@@ -429,15 +847,15 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     }
     lds_barrier();
     for (uint32_t b = 0;; b ^= 1) {
-      const uint32_t n = s_ctl[b][0], stop = s_ctl[b][1];
-      const uint64_t next_pos = pos + s_ctl[b][2], next_vi = vi + s_ctl[b][3];
+      const uint32_t n = uni(s_ctl[b][0]), stop = uni(s_ctl[b][1]);
+      const uint64_t next_pos = pos + uni(s_ctl[b][2]), next_vi = vi + uni(s_ctl[b][3]);
       const bool more = !stop && next_pos < seg_end && next_vi < value_end;
       if (wave == 0) {
         if (more) {  // produce window b^1 while the consumers expand window b
           const uint32_t wrel = (uint32_t)(next_pos - bias) & ~15u;
           fill<kOpt>(s_win[b ^ 1], rs, wrel, kWin, 0, 1, lane);
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          const WalkResult w = walk<kWin>(s_win[b ^ 1], s_off[b ^ 1], s_val[b ^ 1], bias + wrel, next_pos,
+          const WalkResult w = walk<kWin, kCap>(s_win[b ^ 1], s_off[b ^ 1], s_val[b ^ 1], bias + wrel, next_pos,
                                           next_vi, seg_end, src_len, value_end, is_signed, err, lane);
           if (lane == 0) {
             s_ctl[b ^ 1][0] = w.n;
@@ -448,8 +866,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         }
       } else {
         for (uint32_t k = wave - 1; k < n; k += kWaves - 1)
-          expand_run<kOpt>(s_win[b], kWin / 4 + 8, s_off[b][k], vi + s_val[b][k], is_signed, value_begin, value_end, dst,
-                           lane);
+          expand_run<kOpt>(s_win[b], kWin / 4 + 8, uni(s_off[b][k]), vi + uni(s_val[b][k]), is_signed, value_begin,
+                           value_end, dst, lane);
       }
       lds_barrier();
       if (stop) return;
@@ -476,12 +894,13 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
   const int sg = is_signed ? 1 : 0;
 
 #define ORCG_K(T, P, O, WKB, PIPE)                                                                   \
-  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW>), grid, block, 0, ctx->stream, d_src, \
+  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN>), grid, block, 0, ctx->stream, d_src, \
                      src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
                      ctx->d_err)
-#define ORCG_KT(O, WKB, PIPE, MWV)                                                   \
+#define ORCG_KT(O, WKB, PIPE, MWV, DNV)                                              \
   do {                                                                              \
     constexpr int MW = MWV;                                                         \
+    constexpr bool DN = DNV;                                                        \
     if (dst_bytes == 8) {                                                           \
       if (positions_mode) ORCG_K(int64_t, true, O, WKB, PIPE);                       \
       else ORCG_K(int64_t, false, O, WKB, PIPE);                                     \
@@ -495,17 +914,23 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
   } while (0)
 
   switch (ctx->rlev2_variant) {
-    case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6); break;  // 21 KB + fast
-    case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1); break;             // 33 KB, 4 WG/CU
+    case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false); break;  // 21 KB + fast
+    case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
+    case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 4, true); break;  // dense-capable, 21 KB
+    case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true); break;  // dense-capable, 13 KB
     default: {
-      // ORCG_RLEV2_TILED picks the window by stream density: wide values
+      // ORCG_RLEV2_TILED picks the instance by stream density: wide values
       // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
       // 33 KB windows (4 WG/CU); narrower ones need more workgroups in
       // flight per CU to keep HBM busy: 21 KB windows (6 WG/CU) + the
-      // predicate-free full-run path. Measured: scripts/ab_rlev2.py.
+      // predicate-free full-run path; below 2 bytes per value the stream may
+      // be made of short runs (low-cardinality columns), so the instance
+      // with the dense (parallel run discovery) mode runs. Measured:
+      // scripts/ab_rlev2.py.
       const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
-      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1);
-      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6);
+      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false);
+      else if (src_len >= 2 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false);
+      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true);
       break;
     }
   }
@@ -515,3 +940,16 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
 }
 
 }  // namespace orcg
+
+#ifdef ORCG_PHASE_PROF
+extern "C" int orcg_debug_phase_counters(unsigned long long* out, int n, int reset) {
+  unsigned long long h[16];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(orcg::g_phase), sizeof(h)) != hipSuccess) return -1;
+  for (int i = 0; i < n && i < 16; ++i) out[i] = h[i];
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(orcg::g_phase), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

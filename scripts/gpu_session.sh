@@ -19,7 +19,7 @@ STEPS="${*:-pytest smoke bench prof}"
 for s in $STEPS; do
   case $s in
     info) run info 60 bash -c "rocm-smi --showproductname; nproc; lscpu | grep 'Model name'" ;;
-    pytest) run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ;;
+    pytest) run pytest_gpu 1200 python -u -m pytest tests -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     pytestcpu) run pytest_cpu 600 python -m pytest tests -m "not gpu" -q ;;
     smoke) run smoke 300 python __graft_entry__.py smoke ;;
     bench) run bench 600 python bench.py ;;

@@ -1,0 +1,165 @@
+"""GPU parity tests for the tiled kernel's dense (short-run) mode: parallel
+run discovery over slabs and lane-per-run expansion through the LDS stage
+(orc_amd/csrc/rlev2_tiled.hip). Streams are made of short
+runs (SHORT_REPEAT-heavy low-cardinality columns, short DIRECT / DELTA runs)
+with long and PATCHED_BASE runs mixed in, so a window switches between the
+serial walk and dense mode. Bit-exact against the CPU oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+DENSE_VARIANTS = [0, 10, 11]  # default (dense instance below 2 B/value), dense 21 KB, dense 13 KB
+
+
+def _short_run_stream(rng, signed, n_target, long_every=0):
+    """Run kinds / lengths / values of a stream dominated by short runs."""
+    vals, kinds, lens = [], [], []
+    total = 0
+    i = 0
+    while total < n_target:
+        i += 1
+        r = rng.random()
+        if long_every and i % long_every == 0:
+            k = int(rng.choice([1, 2, 3]))
+            L = int(rng.integers(100, 513))
+        elif r < 0.7:
+            k, L = 0, int(rng.integers(3, 11))
+        elif r < 0.8:
+            k, L = 1, int(rng.integers(1, 17))
+        elif r < 0.9:
+            k, L = 3, int(rng.integers(1, 17))
+        else:
+            k, L = 3, int(rng.integers(11, 100))  # fixed-delta repeats (W = 0)
+        if k == 0:
+            x = int(rng.integers(-300, 300)) if signed else int(rng.integers(0, 1 << 20))
+            v = [x] * L
+        elif k == 1:
+            w = int(rng.integers(1, 40))
+            lo = -(1 << (w - 1)) if signed else 0
+            v = list(rng.integers(lo, 1 << (w - 1), size=L))
+        elif k == 2:
+            base = int(rng.integers(0, 5000))
+            x = base + rng.integers(0, 200, size=L)
+            npatch = int(rng.integers(1, 6))
+            idx = rng.choice(L, size=npatch, replace=False)
+            x[idx] += rng.integers(1 << 20, 1 << 30, size=npatch)
+            v = list(x)
+        else:
+            start = int(rng.integers(-10 ** 6, 10 ** 6)) if signed else int(rng.integers(10 ** 6, 2 * 10 ** 6))
+            if r >= 0.9 or rng.integers(0, 2):
+                step = 0 if r >= 0.9 else int(rng.integers(-50, 50))
+                x = start + step * np.arange(L)
+            else:
+                d = rng.integers(1, 1000, size=L)
+                d[0] = 0
+                x = start + np.cumsum(d) * (1 if rng.integers(0, 2) else -1)
+            v = list(x)
+        vals += v
+        kinds.append(k)
+        lens.append(L)
+        total += L
+    return np.array(vals, dtype=np.int64), np.array(kinds, dtype=np.uint8), np.array(lens, dtype=np.uint32)
+
+
+def _encode_with_positions(orc, v, signed, kinds, lens, stride):
+    data, offs = orc.encode_runs(v, signed, kinds, lens)
+    n = v.size
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    g = np.arange(0, n, stride)
+    ri = np.searchsorted(starts, g, side="right") - 1
+    pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
+    return data, pos
+
+
+@pytest.mark.parametrize("signed", [True, False])
+@pytest.mark.parametrize("long_every", [0, 40])
+def test_dense_streams_vs_oracle(signed, long_every):
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(5 + long_every + int(signed))
+    v, kinds, lens = _short_run_stream(rng, signed, 400_000, long_every)
+    ctx = orc_amd.default_context(0)
+    for stride in (10_000, 777, 1 << 30):
+        data, pos = _encode_with_positions(orc_amd, v, signed, kinds, lens, stride)
+        if stride == 10_000:
+            want = oracle.rlev2_decode(data.tobytes(), v.size, signed)
+            np.testing.assert_array_equal(want, v)
+        d_src = torch.from_numpy(data).cuda()
+        d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+        for variant in DENSE_VARIANTS + [1]:
+            ctx.set_rlev2_variant(variant)
+            out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, signed, out)
+            ctx.synchronize()
+            got = out.cpu().numpy()
+            assert np.array_equal(got, v), "variant %d stride %d: first mismatch at %d" % (
+                variant, stride, int(np.argmax(got != v)))
+    ctx.set_rlev2_variant(0)
+
+
+def test_dense_subranges_and_narrow_types():
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(99)
+    v, kinds, lens = _short_run_stream(rng, True, 300_000, 25)
+    stride = 10_000
+    data, pos = _encode_with_positions(orc_amd, v, True, kinds, lens, stride)
+    ctx = orc_amd.default_context(0)
+    d_src = torch.from_numpy(data).cuda()
+    d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+    n = v.size
+    for variant in DENSE_VARIANTS:
+        ctx.set_rlev2_variant(variant)
+        for a, b in [(0, 1), (12345, 54321), (n - 7, n), (9_999, 10_001), (3, n - 3)]:
+            o = torch.full((b - a,), -7, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, b - a, True, o, value_begin=a)
+            ctx.synchronize()
+            np.testing.assert_array_equal(o.cpu().numpy(), v[a:b])
+        for dt, tdt in ((np.int32, torch.int32), (np.int16, torch.int16)):
+            o = torch.empty(n, dtype=tdt, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, n, True, o)
+            ctx.synchronize()
+            np.testing.assert_array_equal(o.cpu().numpy(), v.astype(dt))
+    ctx.set_rlev2_variant(0)
+
+
+@pytest.mark.parametrize("case", ["pl0", "pgw", "delta_len", "truncated"])
+@pytest.mark.parametrize("variant", DENSE_VARIANTS)
+def test_dense_errors_match_reference(case, variant):
+    """A corrupt run after thousands of SHORT_REPEAT runs (dense mode is on
+    when the walk reaches it): the values before it decode, the next read
+    raises the reference's message."""
+    import orc_amd
+
+    rng = np.random.default_rng(3)
+    lens = rng.integers(3, 11, size=3000).astype(np.uint32)
+    v = np.repeat(rng.integers(0, 100, size=lens.size), lens).astype(np.int64)
+    good, _ = orc_amd.encode_runs(v, False, np.zeros(lens.size, np.uint8), lens)
+    tail = {
+        "pl0": bytes([0x8E, 0x09, 0x2B, 0x20, 0x07, 0xD0]),
+        "pgw": bytes([0x8E, 0x09, 0x3F, 0xE1, 0x07]) + bytes(64),
+        "delta_len": bytes([0xC2, 0x00, 0x02, 0x02]),
+        "truncated": bytes([0x5E, 0x03, 0x5C]),
+    }[case]
+    data = good.tobytes() + tail
+    n = v.size
+    with pytest.raises(oracle.OracleError) as want:
+        oracle.RleDecoderV2(data, False).next(n + 1)
+    ctx = orc_amd.default_context(0)
+    ctx.set_rlev2_variant(variant)
+    try:
+        dec = orc_amd.create_rle_decoder(data, False)
+        np.testing.assert_array_equal(dec.next(n), v)
+        with pytest.raises(orc_amd.ParseError) as got:
+            dec.next(1)
+        assert str(got.value) == str(want.value)
+    finally:
+        ctx.set_rlev2_variant(0)
