@@ -228,6 +228,21 @@ int orcg_dict_offsets_device(orcg_ctx* ctx, const int64_t* d_lengths, uint64_t d
 int orcg_dict_gather_device(orcg_ctx* ctx, const void* d_indices, int index_width,
                             const uint8_t* d_not_null, uint64_t n, const int64_t* d_offsets,
                             uint64_t dict_size, int64_t* d_start, int64_t* d_length);
+/* Decimal64ColumnReader / Decimal128ColumnReader::next value decode
+ * (c++/src/ColumnReader.cc:1300-1527) over a device-resident DATA stream of
+ * zigzag varints and the values' scales (the decoded SECONDARY stream):
+ * nvalues values rescaled to `scale`. precision <= 18: int64 d_out[nvalues]
+ * ("Decimal scale out of range" past 18 digits, readInt64 :1342-1349);
+ * precision > 18: int64 d_out[2 * nvalues], [hi, lo] per value (orc::Int128).
+ * Fewer varints than nvalues: "Read past end of stream in
+ * Decimal64ColumnReader". Synchronous. */
+int orcg_decimal_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len, const int64_t* d_scales,
+                               uint64_t nvalues, uint32_t precision, int32_t scale, void* d_out);
+/* TimestampColumnReader::next value construction (c++/src/ColumnReader.cc
+ * :318-347) in place: seconds += epoch (1420070400 for UTC writers), nanos
+ * from the trailing-zero code; writer and reader zones with equal rules. */
+int orcg_timestamp_decode_device(orcg_ctx* ctx, int64_t* d_seconds, int64_t* d_nanos, uint64_t n, int64_t epoch);
+
 /* IntegerColumnReader<LongVectorBatch>::next for a whole stripe column
  * (c++/src/ColumnReader.cc:81-104, 224-258): PRESENT (boolean RLE; NULL/0 if
  * the column has no nulls) + DATA (RLEv2) host streams -> not_null[n] and

@@ -20,12 +20,19 @@
  *   FLOAT, DOUBLE                         : double data[n] (DoubleVectorBatch)
  *   STRING, VARCHAR, CHAR, BINARY         : int64 start[n] (blob-relative), int64 length[n],
  *                                           blob = DATA (direct) or DICTIONARY_DATA bytes
+ *   DECIMAL, precision <= 18              : int64 data[n], unscaled at the type's scale
+ *                                           (Decimal64VectorBatch::values)
+ *   DECIMAL, precision > 18               : int64 data[2n], [hi, lo] per value (orc::Int128 layout,
+ *                                           Decimal128VectorBatch::values)
+ *   TIMESTAMP, TIMESTAMP_INSTANT          : int64 data[n] seconds (UTC), int64 secondary[n] nanoseconds
+ *                                           (TimestampVectorBatch::data / nanoseconds)
  *   LIST, MAP                             : int64 offsets[n + 1] (ListVectorBatch::offsets);
  *                                           children hold offsets[n] rows
  *   STRUCT                                : not_null only; children hold n rows
- * Null slots hold 0 (the reference leaves them unspecified). TIMESTAMP,
- * DECIMAL, UNION and TIMESTAMP_INSTANT columns are not decoded by this round
- * (orcg_reader_column returns ORCG_INVALID_ARGUMENT for them).
+ * Null slots hold 0 (the reference leaves them unspecified). Not decoded
+ * (view.decoded == 0): UNION columns, Hive 0.11 decimals (precision 0) and
+ * TIMESTAMP columns whose writer time zone is not UTC (the reference converts
+ * those with the IANA zone rules, Timezone.cc).
  */
 #ifndef ORCG_READER_H
 #define ORCG_READER_H
@@ -75,6 +82,7 @@ typedef struct {
   const int64_t* offsets;  /* device: list / map offsets (n + 1) */
   const uint8_t* blob;     /* device: string bytes */
   uint64_t blob_len;
+  const int64_t* secondary; /* device: TIMESTAMP nanoseconds (TimestampVectorBatch::nanoseconds) */
 } orcg_column_view;
 
 /* Open an ORC file held in host memory (the caller keeps `file` alive until

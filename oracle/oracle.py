@@ -58,6 +58,8 @@ def lib():
             ("orco_rlev1_seek", [vp, u64, u64], i32),
             ("orco_dict_offsets", [vp, u64, vp], None),
             ("orco_dict_gather", [vp, u64, vp, vp, u64, vp, vp], i32),
+            ("orco_decimal_decode", [vp, sz, vp, u64, i32, i32, vp], i32),
+            ("orco_timestamp", [vp, vp, u64, ctypes.c_int64], None),
         ]:
             f = getattr(L, name)
             f.argtypes = args
@@ -190,3 +192,25 @@ def dict_gather(indices, lengths, not_null=None):
     _check(lib().orco_dict_gather(_ptr(indices), indices.size, _ptr(nn), _ptr(offs), lengths.size,
                                   _ptr(start), _ptr(ln)))
     return start, ln
+
+
+def decimal_decode(data, scales, n, scale, wide):
+    """Decimal64/128ColumnReader value decode (orco_decimal_decode): int64[n],
+    or int64[n, 2] of [hi, lo] when wide."""
+    L = lib()
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    sc = np.ascontiguousarray(scales, dtype=np.int64)
+    out = np.zeros((n, 2) if wide else n, dtype=np.int64)
+    if L.orco_decimal_decode(buf.ctypes.data, buf.size, sc.ctypes.data, n, int(scale), int(bool(wide)),
+                             out.ctypes.data) != 0:
+        raise OracleError(L.orco_last_error().decode())
+    return out
+
+
+def timestamp(secs, nanos, epoch=1420070400):
+    """TimestampColumnReader value construction (orco_timestamp): (seconds, nanoseconds)."""
+    L = lib()
+    s = np.array(secs, dtype=np.int64)
+    ns = np.array(nanos, dtype=np.int64)
+    L.orco_timestamp(s.ctypes.data, ns.ctypes.data, s.size, int(epoch))
+    return s, ns

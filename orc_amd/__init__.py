@@ -18,6 +18,7 @@ from .rle import (  # noqa: F401
     create_boolean_rle_decoder,
     create_byte_rle_decoder,
     create_rle_decoder,
+    decimal_decode_device,
     decode_integer_column,
     dict_gather_device,
     dict_offsets_device,
@@ -29,6 +30,7 @@ from .rle import (  # noqa: F401
     rlev1_decode,
     rlev2_decode,
     scatter_not_null_device,
+    timestamp_decode_device,
 )
 
 from .reader import Reader, open_reader  # noqa: F401,E402

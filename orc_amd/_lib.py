@@ -90,6 +90,8 @@ SIGNATURES = [
     ("orcg_scatter_not_null_device", [vp, vp, vp, u64, vp, i32, i32, ctypes.c_int64], i32),
     ("orcg_dict_offsets_device", [vp, vp, u64, vp], i32),
     ("orcg_dict_gather_device", [vp, vp, i32, vp, u64, vp, u64, vp, vp], i32),
+    ("orcg_decimal_decode_device", [vp, vp, u64, vp, u64, ctypes.c_uint32, i32, vp], i32),
+    ("orcg_timestamp_decode_device", [vp, vp, vp, u64, ctypes.c_int64], i32),
     ("orcg_decode_integer_column", [vp, vp, u64, vp, u64, i32, u64, vp, vp], i32),
     ("orcg_probe_copy", [vp, vp, vp, u64, i32], i32),
     ("orcg_rlev2_encode_direct", [vp, u64, i32, i32, vp, u64, ctypes.POINTER(u64), u64, vp], i32),
@@ -113,7 +115,8 @@ class StripeInfo(ctypes.Structure):
 class ColumnView(ctypes.Structure):
     _fields_ = [("type_id", ctypes.c_uint32), ("kind", ctypes.c_uint32), ("encoding", ctypes.c_uint32),
                 ("decoded", ctypes.c_uint32), ("num_elements", u64), ("has_nulls", i32), ("not_null", vp),
-                ("data", vp), ("length", vp), ("offsets", vp), ("blob", vp), ("blob_len", u64)]
+                ("data", vp), ("length", vp), ("offsets", vp), ("blob", vp), ("blob_len", u64),
+                ("secondary", vp)]
 
 
 u32 = ctypes.c_uint32

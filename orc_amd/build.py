@@ -13,7 +13,7 @@ OUT = os.path.join(HERE, "liborcgpu_prof.so" if PROF else "liborcgpu.so")
 OBJ = os.path.join(HERE, "build_prof" if PROF else "build")
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "encoder.cpp"]
+SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "decimal_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "decimal_api.cpp", "encoder.cpp"]
 HEADERS = ["orcg_internal.hh", "rlev2_device.hh", "orc_file.hh", os.path.join("..", "..", "include", "orcg.h"),
            os.path.join("..", "..", "include", "orcg_reader.h")]
 

@@ -247,6 +247,13 @@ __global__ void flag_negative_kernel(const int64_t* __restrict__ v, uint64_t n, 
 
 }  // namespace
 
+// 16-byte elements (Decimal128 values, orc::Int128 layout [hi, lo])
+struct alignas(16) Pair128 {
+  int64_t hi, lo;
+  __host__ __device__ Pair128() : hi(0), lo(0) {}
+  __host__ __device__ explicit Pair128(int64_t f) : hi(f < 0 ? -1 : 0), lo(f) {}
+};
+
 int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,
                    int fill_mode, int64_t fill) {
   if (n == 0) return ORCG_OK;
@@ -270,11 +277,12 @@ int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t 
                          (const T*)d_dense, d_nn, n, (const uint64_t*)d_off, (T*)d_out, (T)fill);      \
   } while (0)
   switch (width) {
+    case 16: ORCG_SC(Pair128); break;
     case 8: ORCG_SC(int64_t); break;
     case 4: ORCG_SC(int32_t); break;
     case 2: ORCG_SC(int16_t); break;
     case 1: ORCG_SC(int8_t); break;
-    default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "width must be 8, 4, 2 or 1");
+    default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "width must be 16, 8, 4, 2 or 1");
   }
 #undef ORCG_SC
   return hip_check(ctx, hipGetLastError(), "scatter launch");

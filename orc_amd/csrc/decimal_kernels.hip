@@ -1,0 +1,313 @@
+// Decimal and timestamp column kernels (gfx950).
+//
+// Decimal64ColumnReader / Decimal128ColumnReader::next (c++/src/ColumnReader.cc
+// :1300-1527): the DATA stream is a sequence of zigzag base-128 varints (one
+// per non-null value, no run structure), the SECONDARY stream holds each
+// value's scale (signed RLE, decoded by the RLE kernels). A value is rescaled
+// to the column's scale: Decimal64 multiplies / divides by a power of ten
+// (readInt64 :1329-1350, "Decimal scale out of range" past 18 digits),
+// Decimal128 loops in steps of 10^18 (scaleInt128 :1439-1456).
+//
+// Varints have no headers to walk, so the stream is cut anywhere: the grid
+// covers it in 16 KB tiles; pass 1 counts terminator bytes (< 0x80) per tile,
+// an exclusive scan gives every tile its first value index, pass 2 stages the
+// tile (plus 64 bytes of look-back) in LDS, every thread decodes the varints
+// that END in its 64 bytes (a varint that starts in a neighbour's bytes is
+// assembled from the look-back), rescales and stores them at their index.
+//
+// TimestampColumnReader::next (:308-349): seconds (signed RLE) + the writer
+// time zone's epoch, nanos (unsigned RLE) with the trailing-zero code in the
+// low 3 bits; writer and reader in the same (or a rule-free) zone.
+#include "orcg_internal.hh"
+
+namespace orcg {
+namespace {
+
+constexpr int kVThreads = 256;
+constexpr uint32_t kVTile = 16384;
+constexpr uint32_t kVPer = kVTile / kVThreads;  // 64 bytes per thread
+constexpr uint32_t kLook = 64;                 // look-back bytes staged before the tile
+
+__device__ const int64_t kPow10[19] = {1LL,
+                                       10LL,
+                                       100LL,
+                                       1000LL,
+                                       10000LL,
+                                       100000LL,
+                                       1000000LL,
+                                       10000000LL,
+                                       100000000LL,
+                                       1000000000LL,
+                                       10000000000LL,
+                                       100000000000LL,
+                                       1000000000000LL,
+                                       10000000000000LL,
+                                       100000000000000LL,
+                                       1000000000000000LL,
+                                       10000000000000000LL,
+                                       100000000000000000LL,
+                                       1000000000000000000LL};
+
+__device__ __forceinline__ uint32_t term_bits(uint32_t w) {
+  // bit i = byte i of w is a varint terminator (< 0x80)
+  const uint32_t m = (~w >> 7) & 0x01010101u;
+  return (m * 0x10204080u) >> 28;
+}
+
+__global__ __launch_bounds__(kVThreads) void varint_count_kernel(const uint8_t* __restrict__ src, uint64_t len,
+                                                                 int64_t* __restrict__ counts) {
+  const uint64_t t0 = (uint64_t)blockIdx.x * kVTile;
+  uint32_t c = 0;
+  for (uint32_t o = threadIdx.x * 4u; o < kVTile; o += kVThreads * 4u) {
+    const uint64_t p = t0 + o;
+    if (p + 4 <= len) {
+      uint32_t w;
+      __builtin_memcpy(&w, src + p, 4);
+      c += __builtin_popcount(term_bits(w));
+    } else {
+      for (uint64_t q = p; q < len && q < p + 4; ++q) c += src[q] < 0x80u;
+    }
+  }
+  // block reduction
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor((int)c, m);
+  __shared__ uint32_t s[kVThreads / 64];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = (int64_t)(s[0] + s[1] + s[2] + s[3]);
+}
+
+struct U128 {
+  uint64_t lo, hi;
+};
+
+__device__ __forceinline__ U128 mul128_u64(U128 a, uint64_t b) {
+  // (a * b) mod 2^128
+  const uint64_t lo = a.lo * b;
+  const uint64_t hi = __umul64hi(a.lo, b) + a.hi * b;
+  return U128{lo, hi};
+}
+
+// |a| / d for d < 2^32, in 32-bit limbs (Int128 singleDivide, Int128.cc:271-286)
+__device__ __forceinline__ U128 div128_u32(U128 a, uint32_t d) {
+  uint64_t r = 0;
+  uint32_t q[4];
+  const uint32_t limb[4] = {(uint32_t)(a.hi >> 32), (uint32_t)a.hi, (uint32_t)(a.lo >> 32), (uint32_t)a.lo};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r = (r << 32) | limb[j];
+    q[j] = (uint32_t)(r / d);
+    r %= d;
+  }
+  return U128{((uint64_t)q[2] << 32) | q[3], ((uint64_t)q[0] << 32) | q[1]};
+}
+
+__device__ __forceinline__ U128 neg128(U128 a) {
+  const uint64_t lo = ~a.lo + 1;
+  return U128{lo, ~a.hi + (lo == 0 ? 1 : 0)};
+}
+
+// value / 10^k, truncated toward zero (Int128::divide sign rules, :288-...),
+// k <= 18, as two divisions by factors below 2^32
+__device__ __forceinline__ U128 div128_pow10(U128 v, uint32_t k) {
+  const bool neg = (int64_t)v.hi < 0;
+  U128 m = neg ? neg128(v) : v;
+  const uint32_t k1 = k > 9 ? 9 : k, k2 = k - k1;
+  m = div128_u32(m, (uint32_t)kPow10[k1]);
+  if (k2) m = div128_u32(m, (uint32_t)kPow10[k2]);
+  return neg ? neg128(m) : m;
+}
+
+// kMode 0: Decimal64 (int64 out, readInt64); 1: Decimal128 ([hi, lo] int64
+// pairs = orc::Int128's layout, readInt128)
+template <int kMode>
+__global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
+    const uint8_t* __restrict__ src, uint64_t len, const int64_t* __restrict__ tile_base,
+    const int64_t* __restrict__ scales, uint64_t nvalues, int32_t col_scale, void* __restrict__ out,
+    unsigned long long* err) {
+  __shared__ uint32_t s_buf[(kLook + kVTile) / 4 + 1];
+  __shared__ uint32_t s_wsum[kVThreads / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kVTile;
+  const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // stage [t0 - kLook, t0 + kVTile) (zero past the stream; bytes before 0 are
+  // marked as terminators so the first varint starts at 0)
+  for (uint32_t o = (uint32_t)tid * 4u; o < kLook + kVTile; o += kVThreads * 4u) {
+    const int64_t p = (int64_t)t0 - (int64_t)kLook + o;
+    uint32_t w = 0;
+    if (p >= 0 && (uint64_t)p + 4 <= len) {
+      __builtin_memcpy(&w, src + p, 4);
+    } else {
+      for (int i = 0; i < 4; ++i) {
+        const int64_t q = p + i;
+        const uint32_t b = q < 0 ? 0u : ((uint64_t)q < len ? src[q] : 0x80u);
+        w |= b << (8 * i);
+      }
+    }
+    s_buf[o / 4] = w;
+  }
+  __syncthreads();
+  const uint32_t r0 = kLook + (uint32_t)tid * kVPer;  // my bytes in s_buf
+  uint32_t mine[kVPer / 4];
+  uint64_t tmask = 0;
+#pragma unroll
+  for (int i = 0; i < (int)kVPer / 4; ++i) {
+    mine[i] = s_buf[r0 / 4 + i];
+    tmask |= (uint64_t)term_bits(mine[i]) << (4 * i);
+  }
+  // bytes past the end of the stream are not terminators
+  const uint64_t my0 = t0 + (uint64_t)tid * kVPer;
+  if (my0 + kVPer > len) tmask &= my0 >= len ? 0ull : ((1ull << (len - my0)) - 1);
+  const uint32_t cnt = __builtin_popcountll(tmask);
+  // index of my first varint: tile base + exclusive scan of the counts
+  uint32_t incl = cnt;
+  for (int m = 1; m < 64; m <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, m);
+    if (lane >= m) incl += y;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  uint64_t k = (uint64_t)tile_base[blockIdx.x] + (incl - cnt);
+  for (int w = 0; w < wave; ++w) k += s_wsum[w];
+  if (!cnt || k >= nvalues) return;
+
+  // the varint ending at my first terminator starts after the previous
+  // terminator: look back (staged bytes first, then global memory)
+  uint64_t acc_lo = 0, acc_hi = 0;
+  uint32_t shift = 0;
+  auto push = [&](uint32_t b) {
+    const uint64_t x = b & 0x7fu;
+    if constexpr (kMode == 0) {
+      acc_lo |= x << (shift & 63u);  // x86 shift-count masking of readInt64's UB shift
+    } else {
+      if (shift < 64) {
+        acc_lo |= x << shift;
+        if (shift > 57) acc_hi |= x >> (64 - shift);
+      } else if (shift < 128) {
+        acc_hi |= x << (shift - 64);
+      }
+    }
+    shift += 7;
+  };
+  {
+    // first byte of the varint: scan back over continuation bytes
+    int64_t s = (int64_t)my0 - 1;
+    uint32_t back = 0;
+    for (;;) {
+      if (s < 0) break;
+      uint32_t b;
+      const int64_t rel = s - ((int64_t)t0 - (int64_t)kLook);
+      if (rel >= 0) b = (s_buf[rel >> 2] >> ((rel & 3) * 8)) & 0xffu;
+      else b = src[s];
+      if (b < 0x80u) break;
+      --s;
+      ++back;
+    }
+    for (uint64_t q = (uint64_t)(s + 1); q < my0; ++q) {
+      const int64_t rel = (int64_t)q - ((int64_t)t0 - (int64_t)kLook);
+      const uint32_t b = rel >= 0 ? (s_buf[rel >> 2] >> ((rel & 3) * 8)) & 0xffu : src[q];
+      push(b);
+    }
+    (void)back;
+  }
+#pragma unroll
+  for (int i = 0; i < (int)kVPer; ++i) {
+    const uint32_t b = (mine[i >> 2] >> ((i & 3) * 8)) & 0xffu;
+    push(b);
+    if ((tmask >> i) & 1ull) {
+      if (k < nvalues) {
+        const int32_t cur = (int32_t)scales[k];
+        if constexpr (kMode == 0) {
+          int64_t v = (int64_t)((acc_lo >> 1) ^ (0 - (acc_lo & 1)));
+          if (col_scale > cur && (uint64_t)(uint32_t)(col_scale - cur) <= 18) {
+            v = (int64_t)((uint64_t)v * (uint64_t)kPow10[col_scale - cur]);
+          } else if (col_scale < cur && (uint64_t)(uint32_t)(cur - col_scale) <= 18) {
+            v /= kPow10[cur - col_scale];
+          } else if (col_scale != cur) {
+            atomicMin(err, (unsigned long long)((k << 8) | kErrDecimalScale));
+          }
+          ((int64_t*)out)[k] = v;
+        } else {
+          // unZigZagInt128 (:1291-1298): logical >> 1, negate and - 1 if odd
+          const bool odd = acc_lo & 1;
+          U128 v{(acc_lo >> 1) | (acc_hi << 63), acc_hi >> 1};
+          if (odd) {
+            v = neg128(v);
+            const uint64_t lo = v.lo - 1;
+            v.hi -= (v.lo == 0) ? 1 : 0;
+            v.lo = lo;
+          }
+          // scaleInt128 (:1439-1456) with unsigned scales
+          uint32_t s = (uint32_t)col_scale, c = (uint32_t)cur;
+          if (s > c) {
+            while (s > c && (v.lo | v.hi)) {
+              const uint32_t a = min(18u, s - c);
+              v = mul128_u64(v, (uint64_t)kPow10[a]);
+              c += a;
+            }
+          } else {
+            while (c > s && (v.lo | v.hi)) {
+              const uint32_t a = min(18u, c - s);
+              v = div128_pow10(v, a);
+              c -= a;
+            }
+          }
+          int64_t* o = (int64_t*)out + 2 * k;
+          o[0] = (int64_t)v.hi;
+          o[1] = (int64_t)v.lo;
+        }
+      }
+      ++k;
+      acc_lo = acc_hi = 0;
+      shift = 0;
+    }
+  }
+}
+
+// TimestampColumnReader::next (ColumnReader.cc:318-347) for writer == reader
+// time zone rules (no adjustment): secs += epoch; nanos decoded from the
+// trailing-zero code; one second back for negative times with nanos > 999999.
+__global__ __launch_bounds__(256) void timestamp_kernel(int64_t* __restrict__ secs, int64_t* __restrict__ nanos,
+                                                         uint64_t n, int64_t epoch) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  int64_t nv = nanos[i];
+  const uint64_t zeros = (uint64_t)nv & 7u;
+  nv >>= 3;
+  if (zeros != 0)
+    for (uint64_t j = 0; j <= zeros; ++j) nv *= 10;
+  int64_t t = secs[i] + epoch;
+  if (t < 0 && nv > 999999) t -= 1;
+  secs[i] = t;
+  nanos[i] = nv;
+}
+
+}  // namespace
+
+int launch_varint_tile_counts(Ctx* ctx, const uint8_t* d_src, uint64_t len, int64_t* d_counts, uint64_t* ntiles) {
+  *ntiles = (len + kVTile - 1) / kVTile;
+  if (*ntiles == 0) return ORCG_OK;
+  hipLaunchKernelGGL(varint_count_kernel, dim3((unsigned)*ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
+                     d_counts);
+  return hip_check(ctx, hipGetLastError(), "varint_count_kernel launch");
+}
+
+int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
+                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, bool wide, void* d_out) {
+  const uint64_t ntiles = (len + kVTile - 1) / kVTile;
+  if (ntiles == 0 || nvalues == 0) return ORCG_OK;
+  if (wide)
+    hipLaunchKernelGGL(varint_decimal_kernel<1>, dim3((unsigned)ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
+                       d_tile_base, d_scales, nvalues, scale, d_out, ctx->d_err);
+  else
+    hipLaunchKernelGGL(varint_decimal_kernel<0>, dim3((unsigned)ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
+                       d_tile_base, d_scales, nvalues, scale, d_out, ctx->d_err);
+  return hip_check(ctx, hipGetLastError(), "varint_decimal_kernel launch");
+}
+
+int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, int64_t epoch) {
+  if (n == 0) return ORCG_OK;
+  hipLaunchKernelGGL(timestamp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, d_secs, d_nanos,
+                     n, epoch);
+  return hip_check(ctx, hipGetLastError(), "timestamp_kernel launch");
+}
+
+}  // namespace orcg

@@ -23,6 +23,7 @@ const char* dev_error_message(uint32_t code) {
     case kErrByteBadRead: return "bad read in nextBuffer";
     case kErrDictIndex: return "Entry index out of range in StringDictionaryColumn";
     case kErrV1BadRead: return "bad read in readByte";
+    case kErrDecimalScale: return "Decimal scale out of range";
   }
   return "unknown device error";
 }

@@ -24,6 +24,7 @@ enum DevErr : uint32_t {
   kErrByteBadRead = 6,     // "bad read in nextBuffer" (ByteRLE.cc:364)
   kErrDictIndex = 7,       // "Entry index out of range in StringDictionaryColumn" (ColumnReader.cc:578)
   kErrV1BadRead = 8,       // "bad read in readByte" (RLEv1.cc:141-146)
+  kErrDecimalScale = 9,    // "Decimal scale out of range" (ColumnReader.cc:1348)
 };
 
 const char* dev_error_message(uint32_t code);
@@ -76,6 +77,15 @@ int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t 
 int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets);
 int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t* d_nn, uint64_t n,
                        const int64_t* d_offsets, uint64_t dict_size, int64_t* d_start, int64_t* d_len);
+
+// Varint decimals (decimal_kernels.hip): per-16-KB-tile terminator counts,
+// then (after an exclusive scan of the counts) the decode + rescale into
+// int64 (Decimal64) or [hi, lo] int64 pairs (Decimal128, orc::Int128 layout).
+int launch_varint_tile_counts(Ctx* ctx, const uint8_t* d_src, uint64_t len, int64_t* d_counts, uint64_t* ntiles);
+int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
+                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, bool wide, void* d_out);
+// TimestampColumnReader value construction, in place.
+int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, int64_t epoch);
 
 // Multi-workgroup exclusive scan: d_out[0..n] (n + 1 entries). Scratch 7.
 int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out);

@@ -68,9 +68,30 @@ bool is_string_kind(uint32_t k) {
 bool is_int_kind(uint32_t k) {
   return k == ORCG_TYPE_SHORT || k == ORCG_TYPE_INT || k == ORCG_TYPE_LONG || k == ORCG_TYPE_DATE;
 }
-bool is_supported(uint32_t k) {
-  return k != ORCG_TYPE_TIMESTAMP && k != ORCG_TYPE_UNION && k != ORCG_TYPE_DECIMAL &&
-         k != ORCG_TYPE_TIMESTAMP_INSTANT && k <= ORCG_TYPE_CHAR;
+// Zones whose rules are UTC: TIMESTAMP columns written in them decode with
+// no adjustment against the default reader zone, GMT (ColumnReader.cc:333-345
+// is a no-op; epoch 2015-01-01 00:00:00 UTC = 1420070400). Other writer
+// zones need the IANA rules (Timezone.cc) and are not decoded.
+bool utc_zone(const std::string& z) {
+  static const char* kUtc[] = {"GMT", "UTC", "UCT", "Zulu", "Universal", "Greenwich", "GMT0", "GMT+0", "GMT-0",
+                               "Etc/GMT", "Etc/UTC", "Etc/UCT", "Etc/Zulu", "Etc/Universal", "Etc/Greenwich",
+                               "Etc/GMT0", "Etc/GMT+0", "Etc/GMT-0"};
+  for (const char* u : kUtc)
+    if (z == u) return true;
+  return false;
+}
+constexpr int64_t kOrcEpochUtc = 1420070400;
+
+// Columns this reader decodes: every primitive, list / map / struct, decimals
+// with a precision (Hive 0.11 precision-0 decimals are not), timestamps of
+// UTC writers. Not: UNION.
+bool is_supported(const file::TypeInfo& t, const std::string& writer_tz) {
+  const uint32_t k = t.kind;
+  if (k == ORCG_TYPE_UNION) return false;
+  if (k == ORCG_TYPE_DECIMAL) return t.precision != 0;
+  if (k == ORCG_TYPE_TIMESTAMP) return utc_zone(writer_tz);
+  if (k == ORCG_TYPE_TIMESTAMP_INSTANT) return true;
+  return k <= ORCG_TYPE_CHAR || k == ORCG_TYPE_DATE || k == ORCG_TYPE_VARCHAR;
 }
 
 // Caching device allocator: blocks are recycled stripe to stripe.
@@ -128,10 +149,12 @@ struct Col {
   uint8_t* blob = nullptr;
   uint64_t blob_len = 0;
   uint64_t dict_size = 0;  // ColumnEncoding.dictionarySize of this stripe
-  StreamBuf s[4];  // PRESENT, DATA, LENGTH, DICTIONARY_DATA
+  bool supported = false;  // decoded by this reader (is_supported for this stripe's writer zone)
+  int64_t* secondary = nullptr;  // TIMESTAMP nanoseconds
+  StreamBuf s[5];  // PRESENT, DATA, LENGTH, DICTIONARY_DATA, SECONDARY
 };
 
-enum { kSlotPresent = 0, kSlotData = 1, kSlotLength = 2, kSlotDict = 3 };
+enum { kSlotPresent = 0, kSlotData = 1, kSlotLength = 2, kSlotDict = 3, kSlotSecondary = 4 };
 
 int slot_of(uint32_t stream_kind) {
   switch (stream_kind) {
@@ -139,6 +162,7 @@ int slot_of(uint32_t stream_kind) {
     case kData: return kSlotData;
     case kLength: return kSlotLength;
     case kDictionaryData: return kSlotDict;
+    case kSecondary: return kSlotSecondary;
   }
   return -1;
 }
@@ -190,6 +214,7 @@ struct ColOut {
   const int64_t* offsets = nullptr;
   const uint8_t* blob = nullptr;
   uint64_t blob_len = 0;
+  const int64_t* secondary = nullptr;
 };
 
 // One decoded stripe in HBM: its device allocations and column views.
@@ -211,6 +236,7 @@ struct orcg_reader {
   std::vector<uint8_t> selected;  // per type id
   std::string last_error;
   HostStage stages[2];
+  bool decimal_as_long = false;  // PostScript version 1.9999 (UNSTABLE-PRE-2.0): Decimal64V2 columns (Reader.cc:1693-1699)
   std::vector<std::unique_ptr<DevSlot>> slots;  // results of the last read, in stripe order
   size_t nslots = 0;
   // decode() state: the host stage and device slot of the stripe being decoded
@@ -234,7 +260,9 @@ struct orcg_reader {
   int read_stripes(uint64_t first, uint64_t count);
   int upload_and_decode(HostStage& hs, DevSlot& ds);
   int decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count);
-  int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out);
+  // RLE integer stream: v1 for DIRECT / DICTIONARY encodings (convertRleVersion,
+  // DictionaryLoader.hh:42) unless force_v2 (Decimal64ColumnReaderV2 is always RLEv2)
+  int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out, bool force_v2 = false);
   int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out);
   int nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out);
   int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
@@ -257,6 +285,7 @@ int orcg_reader::open_tail() {
   if (!parse_postscript(file + file_len - 1 - ps_len, ps_len, ps))
     return fail(ORCG_PARSE_ERROR, "Failed to parse the postscript");
   if (ps.block_size == 0) ps.block_size = 256 * 1024;
+  decimal_as_long = ps.version.size() == 2 && ps.version[0] == 1 && ps.version[1] == 9999;
   const uint64_t tail = 1 + ps_len + ps.footer_length;
   if (tail >= file_len)
     return fail(ORCG_PARSE_ERROR, "Invalid tail size: footerSize=" + std::to_string(ps.footer_length) +
@@ -303,12 +332,12 @@ int orcg_reader::scatter(const void* dense, const uint8_t* nn, uint64_t n, void*
   return launch_scatter(ctx, dense, nn, n, out, width, 1, 0);
 }
 
-int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out) {
+int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out, bool force_v2) {
   StreamBuf& sb = c.s[slot];
   if (count == 0) return ORCG_OK;
   if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
+  const bool v1 = !force_v2 && (c.encoding == kDirect || c.encoding == kDictionary);
   if (count > sb.plan->values) {
-    const bool v1 = c.encoding == kDirect || c.encoding == kDictionary;
     const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)(v1 ? kErrV1BadRead : kErrBadRead);
     return fail(dev_error_status(e), dev_error_message(e));
   }
@@ -316,7 +345,7 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   const uint64_t* d_seg = (const uint64_t*)(D->d_stage + sb.seg_off);
   const int sg = is_signed ? 1 : 0;
   int rc;
-  if (c.encoding == kDirect || c.encoding == kDictionary)
+  if (v1)
     rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, sb.plan->segs.size(), 0, count, out, 8);
   else
     rc = launch_rlev2(ctx, d_src, sb.len, sg, d_seg, sb.plan->segs.size(), false, 0, 0, count, out, 8);
@@ -346,7 +375,7 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
 
 int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count) {
   Col& c = H->cols[id];
-  if (!selected[id] || !is_supported(c.kind)) return ORCG_OK;
+  if (!selected[id] || !c.supported) return ORCG_OK;
   c.n = n;
   c.decoded = true;
   int rc;
@@ -380,7 +409,60 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
 
   const uint32_t k = c.kind;
   const bool has_data = c.s[kSlotData].present, has_len = c.s[kSlotLength].present;
-  if (is_int_kind(k)) {
+  const bool has_sec = c.s[kSlotSecondary].present;
+  if (k == ORCG_TYPE_DECIMAL) {
+    const file::TypeInfo& t = footer.types[id];
+    const std::string cid = std::to_string(id);
+    if (decimal_as_long && t.precision <= 18) {
+      // Decimal64ColumnReaderV2 (ColumnReader.cc:1529-1576): RLEv2 unscaled values
+      if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64V2 column. ColumnId=" + cid);
+      ORCG_ALLOC(int64_t, dense, nonnull);
+      if ((rc = int_stream(c, kSlotData, true, nonnull, dense, true))) return rc;
+      if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
+    } else {
+      // Decimal64ColumnReader / Decimal128ColumnReader (:1384-1527): varint
+      // DATA, per-value scales in SECONDARY (signed RLE)
+      if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64Column");
+      if (!has_sec) return fail(ORCG_PARSE_ERROR, "SECONDARY stream not found in Decimal64Column");
+      const bool wide = t.precision > 18;
+      ORCG_ALLOC(int64_t, scales, nonnull);
+      if ((rc = int_stream(c, kSlotSecondary, true, nonnull, scales))) return rc;
+      const StreamBuf& sb = c.s[kSlotData];
+      const uint8_t* d_src = D->d_stage + sb.host_off;
+      uint64_t ntiles = 0;
+      ORCG_ALLOC(int64_t, counts, sb.len / 16384 + 2);
+      ORCG_ALLOC(int64_t, base, sb.len / 16384 + 3);
+      if ((rc = launch_varint_tile_counts(ctx, d_src, sb.len, counts, &ntiles))) return fail_ctx(rc);
+      if ((rc = launch_exclusive_scan(ctx, counts, ntiles, base))) return fail_ctx(rc);
+      uint64_t total = 0;
+      if ((rc = hip_check(ctx, hipMemcpyAsync(&total, base + ntiles, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
+          (rc = sync_ctx(ctx)))
+        return fail_ctx(rc);
+      if (total < nonnull)
+        return fail(ORCG_PARSE_ERROR, "Read past end of stream in Decimal64ColumnReader column " + cid + " kind DATA");
+      ORCG_ALLOC(int64_t, dense, wide ? 2 * nonnull : nonnull);
+      if ((rc = launch_varint_decimal(ctx, d_src, sb.len, base, scales, nonnull, (int32_t)t.scale, wide, dense)) ||
+          (rc = sync_ctx(ctx)))
+        return fail_ctx(rc);
+      if (!row_nn) {
+        c.data = dense;
+      } else {
+        ORCG_ALLOC(int64_t, out, wide ? 2 * n : n);
+        if ((rc = scatter(dense, row_nn, n, out, wide ? 16 : 8))) return fail_ctx(rc);
+        c.data = out;
+      }
+    }
+  } else if (k == ORCG_TYPE_TIMESTAMP || k == ORCG_TYPE_TIMESTAMP_INSTANT) {
+    // TimestampColumnReader (:259-349): seconds (signed RLE), nanos (unsigned RLE)
+    if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Timestamp column");
+    if (!has_sec) return fail(ORCG_PARSE_ERROR, "SECONDARY stream not found in Timestamp column");
+    ORCG_ALLOC(int64_t, secs, nonnull);
+    ORCG_ALLOC(int64_t, nanos, nonnull);
+    if ((rc = int_stream(c, kSlotData, true, nonnull, secs))) return rc;
+    if ((rc = int_stream(c, kSlotSecondary, false, nonnull, nanos))) return rc;
+    if ((rc = launch_timestamp(ctx, secs, nanos, nonnull, kOrcEpochUtc))) return fail_ctx(rc);
+    if (!(c.data = place_i64(secs)) || !(c.secondary = place_i64(nanos))) return fail_ctx(ORCG_DEVICE_ERROR);
+  } else if (is_int_kind(k)) {
     if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Integer column");
     ORCG_ALLOC(int64_t, dense, nonnull);
     if ((rc = int_stream(c, kSlotData, true, nonnull, dense))) return rc;
@@ -535,6 +617,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     hs.cols[i].kind = footer.types[i].kind;
     hs.cols[i].encoding = sf.encodings[i].kind;
     hs.cols[i].dict_size = sf.encodings[i].dictionary_size;
+    hs.cols[i].supported = is_supported(footer.types[i], sf.writer_timezone);
   }
   struct Need {
     uint32_t col;
@@ -547,7 +630,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     const StreamInfo& st = sf.streams[i];
     const int slot = slot_of(st.kind);
     if (slot < 0 || st.column >= nt) continue;
-    if (!selected[st.column] || !is_supported(hs.cols[st.column].kind)) continue;
+    if (!selected[st.column] || !hs.cols[st.column].supported) continue;
     if (st.offset + st.length > data_end)
       return hs.fail(ORCG_PARSE_ERROR, "Malformed stream meta at stream index " + std::to_string(i) + " in stripe " +
                                            std::to_string(s));
@@ -598,19 +681,21 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   std::vector<int> rle_kind;  // 0 byte RLE, 1 RLEv1, 2 RLEv2
   for (size_t i = 0; i < nt; ++i) {
     Col& c = hs.cols[i];
-    if (!selected[i] || !is_supported(c.kind)) continue;
+    if (!selected[i] || !c.supported) continue;
     const bool v1 = c.encoding == kDirect || c.encoding == kDictionary;
-    for (int sl = 0; sl < 3; ++sl) {
+    for (int sl : {kSlotPresent, kSlotData, kSlotLength, kSlotSecondary}) {
       StreamBuf& sb = c.s[sl];
       if (!sb.present) continue;
       int kind;
       if (sl == kSlotPresent) kind = 0;
       else if (sl == kSlotData) {
         if (c.kind == ORCG_TYPE_BOOLEAN || c.kind == ORCG_TYPE_BYTE) kind = 0;
-        else if (is_int_kind(c.kind) ||
+        else if (is_int_kind(c.kind) || c.kind == ORCG_TYPE_TIMESTAMP || c.kind == ORCG_TYPE_TIMESTAMP_INSTANT ||
                  (is_string_kind(c.kind) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)))
           kind = v1 ? 1 : 2;
-        else continue;  // raw bytes
+        else if (c.kind == ORCG_TYPE_DECIMAL && decimal_as_long && footer.types[i].precision <= 18)
+          kind = 2;  // Decimal64ColumnReaderV2: RLEv2 (ColumnReader.cc:1544-1556)
+        else continue;  // raw bytes / varints
       } else {
         kind = v1 ? 1 : 2;
       }
@@ -677,6 +762,7 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
     o.offsets = c.offsets;
     o.blob = c.blob;
     o.blob_len = c.blob_len;
+    o.secondary = c.secondary;
   }
   H = nullptr;
   D = nullptr;
@@ -871,7 +957,7 @@ int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t id, orc
   out->kind = r->footer.types[id].kind;
   out->encoding = c.encoding;
   out->decoded = c.decoded ? 1u : 0u;
-  if (!c.decoded) return is_supported(out->kind) ? ORCG_OK : ORCG_INVALID_ARGUMENT;
+  if (!c.decoded) return ORCG_OK;  // not selected, or not decodable (view.decoded == 0)
   out->num_elements = c.n;
   out->has_nulls = c.has_nulls ? 1 : 0;
   out->not_null = c.nn;
@@ -880,6 +966,7 @@ int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t id, orc
   out->offsets = c.offsets;
   out->blob = c.blob;
   out->blob_len = c.blob_len;
+  out->secondary = c.secondary;
   return ORCG_OK;
 }
 

@@ -923,13 +923,15 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
       // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
       // 33 KB windows (4 WG/CU); narrower ones need more workgroups in
       // flight per CU to keep HBM busy: 21 KB windows (6 WG/CU) + the
-      // predicate-free full-run path; below 2 bytes per value the stream may
-      // be made of short runs (low-cardinality columns), so the instance
-      // with the dense (parallel run discovery) mode runs. Measured:
-      // scripts/ab_rlev2.py.
+      // predicate-free full-run path; below 1.25 bytes per value the stream
+      // may be made of short runs (low-cardinality columns: SHORT_REPEAT runs
+      // are 0.2-1 B/value), so the instance with the dense (parallel run
+      // discovery) mode runs: 5x faster on such streams, <= 15 % slower on
+      // narrow long-run streams (its LDS allows 5 WG/CU, not 6). Measured:
+      // scripts/ab_rlev2.py, profiles/r01/sweep.md.
       const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
       if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false);
-      else if (src_len >= 2 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false);
+      else if (4 * src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false);
       else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true);
       break;
     }

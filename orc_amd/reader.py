@@ -12,6 +12,7 @@ tests.
 """
 import ctypes
 import datetime
+import decimal
 
 import numpy as np
 
@@ -49,8 +50,9 @@ class Type:
 class ColumnBatch:
     """Host copy of one column's device batch."""
 
-    def __init__(self, kind, n, not_null, data, length, offsets, blob, encoding):
+    def __init__(self, kind, n, not_null, data, length, offsets, blob, encoding, secondary=None):
         self.kind = kind
+        self.secondary = secondary  # np.int64[n] TIMESTAMP nanoseconds
         self.num_elements = n
         self.not_null = not_null  # np.uint8[n] or None
         self.data = data          # np.int64 / np.float64 [n] (string starts for string kinds)
@@ -87,6 +89,17 @@ class Batch:
             return _EPOCH + datetime.timedelta(days=int(c.data[i]))
         if k in (FLOAT, DOUBLE):
             return float(c.data[i])
+        if k == DECIMAL:
+            # Decimal64VectorBatch int64 / Decimal128VectorBatch [hi, lo]
+            if t.precision > 18:
+                hi, lo = int(c.data[2 * i]), int(c.data[2 * i + 1]) & ((1 << 64) - 1)
+                u = (hi << 64) | lo
+            else:
+                u = int(c.data[i])
+            return decimal.Decimal(u).scaleb(-t.scale)
+        if k in (TIMESTAMP, TIMESTAMP_INSTANT):
+            # TimestampVectorBatch seconds + nanoseconds, as numpy datetime64[ns]
+            return np.datetime64(int(c.data[i]) * 1_000_000_000 + int(c.secondary[i]), "ns")
         if k in (STRING, VARCHAR, CHAR, BINARY):
             s, ln = int(c.data[i]), int(c.length[i])
             raw = c.blob[s:s + ln]
@@ -274,7 +287,13 @@ class Reader:
                 blob = self._host(v.blob, v.blob_len, np.uint8).tobytes()
             elif k in (LIST, MAP):
                 offsets = self._host(v.offsets, 8 * (n + 1), np.int64)
-            cols[t.id] = ColumnBatch(k, n, nn, data, length, offsets, blob, v.encoding)
+            secondary = None
+            if k == DECIMAL:
+                data = self._host(v.data, (16 if t.precision > 18 else 8) * n, np.int64)
+            elif k in (TIMESTAMP, TIMESTAMP_INSTANT):
+                data = self._host(v.data, 8 * n, np.int64)
+                secondary = self._host(v.secondary, 8 * n, np.int64)
+            cols[t.id] = ColumnBatch(k, n, nn, data, length, offsets, blob, v.encoding, secondary)
         return Batch(self, cols)
 
     def last_timings(self):

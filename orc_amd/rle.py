@@ -377,6 +377,24 @@ def dict_gather_device(ctx, indices, offsets, start, length, not_null=None):
     return start, length
 
 
+def decimal_decode_device(ctx, src, scales, nvalues, precision, scale, out, src_len=None):
+    """Decimal64/128ColumnReader value decode of a device varint stream:
+    `out` int64[nvalues] (precision <= 18) or int64[nvalues, 2] [hi, lo]."""
+    L = _lib.load()
+    n = src.numel() if src_len is None else src_len
+    check(L.orcg_decimal_decode_device(ctx.handle, _tensor_ptr(src), n, _tensor_ptr(scales), nvalues, precision,
+                                       scale, _tensor_ptr(out)), ctx.last_error)
+    return out
+
+
+def timestamp_decode_device(ctx, seconds, nanos, epoch=1420070400):
+    """TimestampColumnReader value construction on device tensors, in place."""
+    L = _lib.load()
+    check(L.orcg_timestamp_decode_device(ctx.handle, _tensor_ptr(seconds), _tensor_ptr(nanos), seconds.numel(),
+                                         int(epoch)), ctx.last_error)
+    return seconds, nanos
+
+
 def decode_integer_column(present, data, n, is_signed=True, ctx=None):
     """IntegerColumnReader::next over a stripe column: (values, not_null);
     null slots of `values` stay 0 (untouched)."""

@@ -21,10 +21,14 @@ def ctx():
 
 def _read_all(ctx, name, fields=None):
     r = orc_amd.Reader(path(name), ctx)
-    fields = supported_fields(r) if fields is None else fields
+    batches = [r.read_stripe(s) for s in range(r.num_stripes)]
+    decoded = None
+    for b in batches:
+        decoded = set(b.columns) if decoded is None else decoded & set(b.columns)
+    fields = supported_fields(r, decoded) if fields is None else fields
     rows = []
-    for s in range(r.num_stripes):
-        rows.extend(r.read_stripe(s).to_pylist(fields))
+    for b in batches:
+        rows.extend(b.to_pylist(fields))
     return r, fields, rows
 
 

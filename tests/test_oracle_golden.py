@@ -110,3 +110,48 @@ def test_dict_gather_bounds():
     assert list(start) == [0, 3, 3] and list(ln) == [3, 5, 0]
     with pytest.raises(oracle.OracleError, match="Entry index out of range"):
         oracle.dict_gather([3], [1, 2, 3])
+
+
+DECIMAL = load_golden("kat_decimal.json")
+
+
+def _kat_nonnull(fx):
+    if not fx.get("present"):
+        return len(fx["expected"])
+    dec = oracle.ByteRleDecoder(bytes.fromhex(fx["present"]), boolean=True)
+    return int(np.count_nonzero(dec.next(len(fx["expected"]) * 2 + 64)[: 10 ** 6]))
+
+
+@pytest.mark.parametrize("fx", DECIMAL, ids=[f["name"] for f in DECIMAL])
+def test_decimal_timestamp_kat(fx):
+    """Decimal64/128 and timestamp known answers of TestColumnReader.cc: the
+    SECONDARY stream through the RLEv1 oracle, then the value construction."""
+    n = len(fx["expected"])
+    sec = bytes.fromhex(fx["secondary"])
+    data = bytes.fromhex(fx["data"])
+    if fx["kind"] == "decimal":
+        scales = oracle.RleDecoderV1(sec, True).next(n)
+        wide = fx["precision"] > 18
+        got = oracle.decimal_decode(data, scales, n, fx["scale"], wide)
+        if wide:
+            vals = [(((int(h) & ((1 << 64) - 1)) << 64) | (int(lo) & ((1 << 64) - 1))) for h, lo in got]
+            vals = [v - (1 << 128) if v >> 127 else v for v in vals]
+        else:
+            vals = [int(v) for v in got]
+        assert vals == fx["expected"]
+    else:
+        secs = oracle.RleDecoderV1(data, True).next(n)
+        nanos = oracle.RleDecoderV1(sec, False).next(n)
+        s, ns = oracle.timestamp(secs, nanos)
+        assert list(s) == fx["expected"]
+        assert list(ns) == fx["expected_nanos"]
+
+
+def test_decimal_errors():
+    # varint stream ends early; scale 20 digits away from the column's
+    with pytest.raises(oracle.OracleError, match="Read past end of stream in Decimal64ColumnReader"):
+        oracle.decimal_decode(bytes([6, 0x80]), [2, 2], 2, 2, False)
+    with pytest.raises(oracle.OracleError, match="Decimal scale out of range"):
+        oracle.decimal_decode(bytes([6]), [22], 1, 2, False)
+    # Decimal128 has no range error: 10^-20 of 3 truncates to 0
+    assert oracle.decimal_decode(bytes([6]), [22], 1, 2, True).tolist() == [[0, 0]]
