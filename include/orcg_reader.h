@@ -133,6 +133,10 @@ int orcg_reader_copy_to_host(orcg_reader* r, void* host_dst, const void* device_
  * threads), [3] H2D, [4] device decode. With read_stripes, [0..2] of
  * stripe i + 1 overlap [3..4] of stripe i. */
 int orcg_reader_last_timings(const orcg_reader* r, double* out5);
+/* RLE streams of the last read cut at row groups by the ROW_INDEX positions
+ * (ColumnReader::seekToRowGroup's PositionProvider, no host work) [0] and by
+ * a host header walk (files without a row index) [1]. */
+int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2);
 
 #ifdef __cplusplus
 }

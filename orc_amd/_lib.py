@@ -146,6 +146,7 @@ SIGNATURES += [
     ("orcg_reader_stripe_column", [vp, u64, u32, ctypes.POINTER(ColumnView)], i32),
     ("orcg_reader_copy_to_host", [vp, vp, vp, u64], i32),
     ("orcg_reader_last_timings", [vp, ctypes.POINTER(ctypes.c_double)], i32),
+    ("orcg_reader_last_stream_stats", [vp, ctypes.POINTER(u64)], i32),
 ]
 
 

@@ -112,6 +112,8 @@ __global__ __launch_bounds__(kWave) void byterle_kernel(const uint8_t* __restric
     if (pos > seg_end) { if (lane == 0) report(err, vi, kErrBadSegment); return; }
   }
   if (lane == 0 && v_next != ~0ull && vi * scale < end && vi != v_next) report(err, vi, kErrBadSegment);
+  // the last segment ran out of stream before the requested values
+  if (lane == 0 && v_next == ~0ull && vi * scale < end) report(err, vi, kErrByteBadRead);
 }
 
 }  // namespace

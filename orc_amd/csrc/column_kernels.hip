@@ -245,6 +245,57 @@ __global__ void flag_negative_kernel(const int64_t* __restrict__ v, uint64_t n, 
   if (__any(neg) && (threadIdx.x % kWave) == 0) atomicOr(flag, 1ull);
 }
 
+// ---- row-index segmentation (ColumnReader::seekToRowGroup positions) ----
+// A column's streams are cut at its row groups: the row index gives, per row
+// group g and stream, the run-aligned byte offset of the run holding the row
+// group's first value and the values to skip in it (RleDecoder::seek + skip,
+// c++/src/RleDecoderV2.cc:109-130, ByteRLE.cc:527-560). The value index of
+// that first value is the number of present rows before the row group's
+// first row (in the column's row space), so the segment of g starts at value
+// prefix[g] - skip[g].
+
+// counts[g] = non-zero mask bytes in rows [rows[g], rows[g + 1]) (row n ends the last)
+__global__ __launch_bounds__(kThreads) void rg_count_kernel(const uint8_t* __restrict__ mask, uint64_t n,
+                                                             const int64_t* __restrict__ rows, uint64_t G,
+                                                             int64_t* __restrict__ counts) {
+  __shared__ uint32_t red[kThreads / kWave];
+  const uint64_t g = blockIdx.x;
+  uint64_t a = (uint64_t)rows[g], b = g + 1 < G ? (uint64_t)rows[g + 1] : n;
+  if (a > n) a = n;
+  if (b > n) b = n;
+  uint32_t c = 0;
+  for (uint64_t r = a + threadIdx.x; r < b; r += kThreads) c += mask[r] != 0;
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor((int)c, m);
+  if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kThreads / kWave; ++w) t += red[w];
+    counts[g] = (int64_t)(b > a ? t : 0);
+  }
+}
+
+// seg[g] = {byte offset, first value index of the run at it}. trip[g] =
+// {byte offset, values (bytes for boolean streams) to skip, bits to skip};
+// prefix[g] = values (rows for boolean streams) before the row group.
+__global__ void rg_segtab_kernel(const int64_t* __restrict__ trip, const int64_t* __restrict__ prefix, uint64_t G,
+                                 int boolean, uint64_t* __restrict__ seg) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const int64_t off = trip[3 * g], skip = trip[3 * g + 1], bits = trip[3 * g + 2];
+  int64_t v = boolean ? (prefix[g] - bits) / 8 - skip : prefix[g] - skip;
+  if (v < 0) v = 0;  // a corrupt index: the decode reports the segment mismatch
+  seg[2 * g] = (uint64_t)off;
+  seg[2 * g + 1] = (uint64_t)v;
+}
+
+// child row group starts of a list / map column: offsets[parent rows[g]]
+__global__ void rg_child_rows_kernel(const int64_t* __restrict__ offsets, const int64_t* __restrict__ rows,
+                                     uint64_t G, int64_t* __restrict__ out) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < G) out[g] = offsets[rows[g]];
+}
+
 }  // namespace
 
 // 16-byte elements (Decimal128 values, orc::Int128 layout [hi, lo])
@@ -376,6 +427,35 @@ int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out) 
       return set_error(ctx, ORCG_INVALID_ARGUMENT, "bad widen kind");
   }
   return hip_check(ctx, hipGetLastError(), "widen launch");
+}
+
+}  // namespace orcg
+
+namespace orcg {
+
+int launch_rg_prefix(Ctx* ctx, const uint8_t* d_mask, uint64_t n, const int64_t* d_rows, uint64_t G,
+                     int64_t* d_counts, int64_t* d_prefix) {
+  if (G == 0) return ORCG_OK;
+  if (G > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many row groups");
+  hipLaunchKernelGGL(rg_count_kernel, dim3((unsigned)G), dim3(kThreads), 0, ctx->stream, d_mask, n, d_rows, G,
+                     d_counts);
+  const int rc = hip_check(ctx, hipGetLastError(), "rg_count_kernel launch");
+  return rc ? rc : launch_exclusive_scan(ctx, d_counts, G, d_prefix);
+}
+
+int launch_rg_segtab(Ctx* ctx, const int64_t* d_trip, const int64_t* d_prefix, uint64_t G, bool boolean,
+                     uint64_t* d_seg) {
+  if (G == 0) return ORCG_OK;
+  hipLaunchKernelGGL(rg_segtab_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, ctx->stream, d_trip,
+                     d_prefix, G, boolean ? 1 : 0, d_seg);
+  return hip_check(ctx, hipGetLastError(), "rg_segtab_kernel launch");
+}
+
+int launch_rg_child_rows(Ctx* ctx, const int64_t* d_offsets, const int64_t* d_rows, uint64_t G, int64_t* d_out) {
+  if (G == 0) return ORCG_OK;
+  hipLaunchKernelGGL(rg_child_rows_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, ctx->stream, d_offsets,
+                     d_rows, G, d_out);
+  return hip_check(ctx, hipGetLastError(), "rg_child_rows_kernel launch");
 }
 
 }  // namespace orcg

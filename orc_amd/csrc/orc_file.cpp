@@ -106,6 +106,41 @@ bool parse_type(Pb m, TypeInfo& t) {
   return m.ok;
 }
 
+}  // namespace
+
+bool parse_row_index(const uint8_t* p, uint64_t n, std::vector<std::vector<uint64_t>>& entries) {
+  // message RowIndex { repeated RowIndexEntry entry = 1; }
+  // message RowIndexEntry { repeated uint64 positions = 1 [packed = true];
+  //                         optional ColumnStatistics statistics = 2; }
+  Pb m(p, n);
+  uint32_t f, w;
+  while (m.more() && m.key(f, w)) {
+    if (f == 1 && w == 2) {
+      Pb e = m.bytes();
+      std::vector<uint64_t> pos;
+      uint32_t ef, ew;
+      while (e.more() && e.key(ef, ew)) {
+        if (ef == 1 && ew == 2) {
+          Pb q = e.bytes();
+          while (q.more()) pos.push_back(q.varint());
+          if (!q.ok) return false;
+        } else if (ef == 1 && ew == 0) {
+          pos.push_back(e.varint());
+        } else {
+          e.skip(ew);
+        }
+      }
+      if (!e.ok) return false;
+      entries.push_back(std::move(pos));
+    } else {
+      m.skip(w);
+    }
+  }
+  return m.ok;
+}
+
+namespace {
+
 // ---- snappy (raw block format) -------------------------------------------
 // The reference links libsnappy (SnappyDecompressionStream, Compression.cc);
 // this is the published block format: a varint uncompressed length, then

@@ -89,6 +89,9 @@ struct Chunk {
 bool parse_postscript(const uint8_t* p, uint64_t n, PostScript& ps);
 bool parse_footer(const uint8_t* p, uint64_t n, Footer& f);
 bool parse_stripe_footer(const uint8_t* p, uint64_t n, uint64_t stripe_offset, StripeFooter& sf);
+// RowIndex (orc_proto.proto; ORCv1.md "Indexes"): the positions list of every
+// RowIndexEntry, one per row group.
+bool parse_row_index(const uint8_t* p, uint64_t n, std::vector<std::vector<uint64_t>>& entries);
 
 // Split [off, off + len) of the file into compression chunks (3-byte
 // headers); NONE yields one original chunk. False on a malformed header.

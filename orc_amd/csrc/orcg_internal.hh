@@ -87,6 +87,16 @@ int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const in
 // TimestampColumnReader value construction, in place.
 int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, int64_t epoch);
 
+// Row-index segmentation (column_kernels.hip): prefix[g] = non-zero bytes of
+// mask before row rows[g] (counts: scratch of G entries; prefix: G + 1);
+// segment table from {offset, skip, bit skip} triplets; list / map child row
+// group starts.
+int launch_rg_prefix(Ctx* ctx, const uint8_t* d_mask, uint64_t n, const int64_t* d_rows, uint64_t G,
+                     int64_t* d_counts, int64_t* d_prefix);
+int launch_rg_segtab(Ctx* ctx, const int64_t* d_trip, const int64_t* d_prefix, uint64_t G, bool boolean,
+                     uint64_t* d_seg);
+int launch_rg_child_rows(Ctx* ctx, const int64_t* d_offsets, const int64_t* d_rows, uint64_t G, int64_t* d_out);
+
 // Multi-workgroup exclusive scan: d_out[0..n] (n + 1 entries). Scratch 7.
 int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out);
 // Number of non-zero bytes of d_nn[0..n) into *d_total (device). Scratch 5, 6.

@@ -135,6 +135,11 @@ struct StreamBuf {
   uint64_t len = 0;       // decompressed bytes
   std::unique_ptr<orcg_rlev2_plan> plan;
   uint64_t seg_off = 0;   // offset of the plan's segment table in staging
+  // row-index segmentation: per row group {byte offset, values to skip, bits
+  // to skip} (int64 x 3) in staging at rg_off; no host plan
+  bool pos = false;
+  std::vector<int64_t> trip;
+  uint64_t rg_off = 0;
 };
 
 struct Col {
@@ -180,6 +185,9 @@ struct HostStage {
   int rc = ORCG_OK;
   std::string err;
   double t_parse = 0, t_decomp = 0, t_plan = 0;
+  uint64_t ngroups = 0;    // row groups with row-index positions (0: host plans only)
+  uint64_t n_pos = 0, n_plan = 0;  // RLE streams cut by the row index / by a host plan
+  uint64_t rows_off = 0;   // staging offset of int64 rows[g] = g * stride
   ~HostStage() {
     if (h) (void)hipHostFree(h);
   }
@@ -243,6 +251,7 @@ struct orcg_reader {
   HostStage* H = nullptr;
   DevSlot* D = nullptr;
   double timings[5] = {0, 0, 0, 0, 0};
+  uint64_t stream_stats[2] = {0, 0};  // last read: RLE streams cut by the row index, by host plans
 
   ~orcg_reader() {
     slots.clear();
@@ -259,7 +268,13 @@ struct orcg_reader {
   int prepare(uint64_t s, HostStage& hs) const;
   int read_stripes(uint64_t first, uint64_t count);
   int upload_and_decode(HostStage& hs, DevSlot& ds);
-  int decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count);
+  int decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count, const int64_t* rg_rows);
+  // row-group context of the column being decoded (segments())
+  const int64_t* cur_rows = nullptr;  // device: first row of each row group, in the column's rows
+  uint64_t cur_n = 0;
+  const uint8_t* cur_in_nn = nullptr;
+  const uint8_t* cur_row_nn = nullptr;
+  int segments(Col& c, int slot, bool boolean, const uint64_t** d_seg, uint64_t* nseg);
   // RLE integer stream: v1 for DIRECT / DICTIONARY encodings (convertRleVersion,
   // DictionaryLoader.hh:42) unless force_v2 (Decimal64ColumnReaderV2 is always RLEv2)
   int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out, bool force_v2 = false);
@@ -332,40 +347,6 @@ int orcg_reader::scatter(const void* dense, const uint8_t* nn, uint64_t n, void*
   return launch_scatter(ctx, dense, nn, n, out, width, 1, 0);
 }
 
-int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out, bool force_v2) {
-  StreamBuf& sb = c.s[slot];
-  if (count == 0) return ORCG_OK;
-  if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
-  const bool v1 = !force_v2 && (c.encoding == kDirect || c.encoding == kDictionary);
-  if (count > sb.plan->values) {
-    const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)(v1 ? kErrV1BadRead : kErrBadRead);
-    return fail(dev_error_status(e), dev_error_message(e));
-  }
-  const uint8_t* d_src = D->d_stage + sb.host_off;
-  const uint64_t* d_seg = (const uint64_t*)(D->d_stage + sb.seg_off);
-  const int sg = is_signed ? 1 : 0;
-  int rc;
-  if (v1)
-    rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, sb.plan->segs.size(), 0, count, out, 8);
-  else
-    rc = launch_rlev2(ctx, d_src, sb.len, sg, d_seg, sb.plan->segs.size(), false, 0, 0, count, out, 8);
-  return rc ? fail_ctx(rc) : ORCG_OK;
-}
-
-int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out) {
-  StreamBuf& sb = c.s[slot];
-  if (count == 0) return ORCG_OK;
-  if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
-  const uint64_t avail = boolean ? sb.plan->values * 8 : sb.plan->values;
-  if (count > avail) {
-    const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)kErrByteBadRead;
-    return fail(dev_error_status(e), dev_error_message(e));
-  }
-  const int rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, (const uint64_t*)(D->d_stage + sb.seg_off),
-                                sb.plan->segs.size(), boolean, 0, count, out);
-  return rc ? fail_ctx(rc) : ORCG_OK;
-}
-
 #define ORCG_ALLOC(T, v, count)                                                   \
   T* v = alloc<T>(count);                                                         \
   if (!v) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed")
@@ -373,12 +354,87 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   v = alloc<T>(count);                                                            \
   if (!v) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed")
 
-int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count) {
+// The stream's segment table: the host plan's, or (row-index streams) built
+// on the device from the row groups' positions and the present-row prefix
+// at each row group's first row (PRESENT streams count the incoming rows).
+int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg, uint64_t* nseg) {
+  StreamBuf& sb = c.s[slot];
+  if (!sb.pos) {
+    *d_seg = (const uint64_t*)(D->d_stage + sb.seg_off);
+    *nseg = sb.plan->segs.size();
+    return ORCG_OK;
+  }
+  const uint64_t G = H->ngroups;
+  if (!cur_rows) return fail(ORCG_INVALID_ARGUMENT, "row groups without row starts");
+  const uint8_t* mask = slot == kSlotPresent ? cur_in_nn : cur_row_nn;
+  const int64_t* prefix = cur_rows;
+  int rc;
+  if (mask) {
+    ORCG_ALLOC(int64_t, counts, G);
+    ORCG_ALLOC(int64_t, pre, G + 1);
+    if ((rc = launch_rg_prefix(ctx, mask, cur_n, cur_rows, G, counts, pre))) return fail_ctx(rc);
+    prefix = pre;
+  }
+  ORCG_ALLOC(uint64_t, seg, 2 * G);
+  if ((rc = launch_rg_segtab(ctx, (const int64_t*)(D->d_stage + sb.rg_off), prefix, G, boolean, seg)))
+    return fail_ctx(rc);
+  *d_seg = seg;
+  *nseg = G;
+  return ORCG_OK;
+}
+
+int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out, bool force_v2) {
+  StreamBuf& sb = c.s[slot];
+  if (count == 0) return ORCG_OK;
+  if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
+  const bool v1 = !force_v2 && (c.encoding == kDirect || c.encoding == kDictionary);
+  if (!sb.pos && count > sb.plan->values) {
+    const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)(v1 ? kErrV1BadRead : kErrBadRead);
+    return fail(dev_error_status(e), dev_error_message(e));
+  }
+  const uint8_t* d_src = D->d_stage + sb.host_off;
+  const uint64_t* d_seg;
+  uint64_t nseg;
+  int rc = segments(c, slot, false, &d_seg, &nseg);
+  if (rc) return rc;
+  const int sg = is_signed ? 1 : 0;
+  if (v1)
+    rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
+  else
+    rc = launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
+  return rc ? fail_ctx(rc) : ORCG_OK;
+}
+
+int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out) {
+  StreamBuf& sb = c.s[slot];
+  if (count == 0) return ORCG_OK;
+  if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
+  if (!sb.pos) {
+    const uint64_t avail = boolean ? sb.plan->values * 8 : sb.plan->values;
+    if (count > avail) {
+      const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)kErrByteBadRead;
+      return fail(dev_error_status(e), dev_error_message(e));
+    }
+  }
+  const uint64_t* d_seg;
+  uint64_t nseg;
+  int rc = segments(c, slot, boolean, &d_seg, &nseg);
+  if (rc) return rc;
+  rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out);
+  return rc ? fail_ctx(rc) : ORCG_OK;
+}
+
+
+int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count, const int64_t* rg_rows) {
   Col& c = H->cols[id];
   if (!selected[id] || !c.supported) return ORCG_OK;
   c.n = n;
   c.decoded = true;
   int rc;
+  cur_rows = rg_rows;
+  cur_n = n;
+  cur_in_nn = in_nn;
+  cur_row_nn = nullptr;
   // ColumnReader::next: PRESENT bits for the incoming non-null rows
   uint64_t nonnull = in_nn ? in_count : n;
   uint8_t* nn = nullptr;
@@ -399,6 +455,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   if (in_nn && !c.s[kSlotPresent].present) c.has_nulls = true;  // incoming mask copied (:97-101)
   c.nn = c.has_nulls ? nn : nullptr;
   const uint8_t* row_nn = c.nn;
+  cur_row_nn = row_nn;
 
   auto place_i64 = [&](int64_t* dense) -> int64_t* {
     if (!row_nn) return dense;
@@ -579,11 +636,17 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if ((rc = hip_check(ctx, hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
         (rc = sync_ctx(ctx)))
       return fail_ctx(rc);
+    // the children's row groups start at the list offsets of the parent's
+    int64_t* child_rows = nullptr;
+    if (rg_rows && H->ngroups) {
+      ORCG_ALLOC_TO(int64_t, child_rows, H->ngroups);
+      if ((rc = launch_rg_child_rows(ctx, off, rg_rows, H->ngroups, child_rows))) return fail_ctx(rc);
+    }
     for (uint32_t st : footer.types[id].subtypes)
-      if ((rc = decode(st, total, nullptr, total))) return rc;
+      if ((rc = decode(st, total, nullptr, total, child_rows))) return rc;
   } else if (k == ORCG_TYPE_STRUCT) {
     for (uint32_t st : footer.types[id].subtypes)
-      if ((rc = decode(st, n, c.nn, nonnull))) return rc;
+      if ((rc = decode(st, n, c.nn, nonnull, rg_rows))) return rc;
   }
   return ORCG_OK;
 }
@@ -623,18 +686,23 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     uint32_t col;
     int slot;
     std::vector<Chunk> chunks;
+    uint64_t file_off = 0;  // stream start in the file
   };
+  std::vector<int> row_index(nt, -1);  // ROW_INDEX stream of each column (index into sf.streams)
   std::vector<Need> needs;
   const uint64_t data_end = si.offset + si.index_length + si.data_length;
   for (size_t i = 0; i < sf.streams.size(); ++i) {
     const StreamInfo& st = sf.streams[i];
+    if (st.kind == kRowIndex && st.column < nt && selected[st.column] && hs.cols[st.column].supported &&
+        st.offset + st.length <= data_end)
+      row_index[st.column] = (int)i;
     const int slot = slot_of(st.kind);
     if (slot < 0 || st.column >= nt) continue;
     if (!selected[st.column] || !hs.cols[st.column].supported) continue;
     if (st.offset + st.length > data_end)
       return hs.fail(ORCG_PARSE_ERROR, "Malformed stream meta at stream index " + std::to_string(i) + " in stripe " +
                                            std::to_string(s));
-    Need nd{st.column, slot, {}};
+    Need nd{st.column, slot, {}, st.offset};
     if (!split_chunks(file, st.offset, st.length, ps.compression, nd.chunks, err)) return hs.fail(ORCG_PARSE_ERROR, err);
     needs.push_back(std::move(nd));
   }
@@ -676,6 +744,125 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     sb.len = w - s0;
   }
   const double t15 = now_s();
+  // Row-index segmentation: the positions every row group records for each of
+  // the column's streams (ColumnReader::seekToRowGroup order, ColumnReader.cc;
+  // the writers' recordPosition order, ColumnWriter.cc) give run-aligned cut
+  // points, so those streams need no host header walk.
+  hs.ngroups = 0;
+  // ORCG_NO_ROW_INDEX=1 forces the host plans (A/B and tests)
+  const char* no_ri = getenv("ORCG_NO_ROW_INDEX");
+  if (footer.row_index_stride > 0 && si.num_rows > 0 && !(no_ri && no_ri[0] == '1')) {
+    const uint64_t G = (si.num_rows + footer.row_index_stride - 1) / footer.row_index_stride;
+    std::vector<int> need_of(nt * 5, -1);
+    for (size_t i = 0; i < needs.size(); ++i) need_of[needs[i].col * 5 + needs[i].slot] = (int)i;
+    const bool compressed = ps.compression != kNone;
+    enum { kRaw = 0, kInt = 1, kByteRle = 2, kBool = 3 };
+    // one column per task: decompress + parse its ROW_INDEX, map positions
+    std::atomic<bool> any{false};
+    parallel_for(nt, [&](size_t col) {
+      if (row_index[col] < 0) return;
+      Col& c = hs.cols[col];
+      const uint32_t k = c.kind;
+      std::vector<std::pair<int, int>> order;  // (slot, stream kind)
+      if (c.s[kSlotPresent].present) order.push_back({kSlotPresent, kBool});
+      const bool dict = c.encoding == kDictionary || c.encoding == kDictionaryV2;
+      if (k == ORCG_TYPE_BOOLEAN) order.push_back({kSlotData, kBool});
+      else if (k == ORCG_TYPE_BYTE) order.push_back({kSlotData, kByteRle});
+      else if (is_int_kind(k)) order.push_back({kSlotData, kInt});
+      else if (k == ORCG_TYPE_FLOAT || k == ORCG_TYPE_DOUBLE) order.push_back({kSlotData, kRaw});
+      else if (is_string_kind(k)) {
+        if (dict) order.push_back({kSlotData, kInt});
+        else {
+          order.push_back({kSlotData, kRaw});
+          order.push_back({kSlotLength, kInt});
+        }
+      } else if (k == ORCG_TYPE_DECIMAL) {
+        if (decimal_as_long && footer.types[col].precision <= 18) order.push_back({kSlotData, kInt});
+        else {
+          order.push_back({kSlotData, kRaw});
+          order.push_back({kSlotSecondary, kInt});
+        }
+      } else if (k == ORCG_TYPE_TIMESTAMP || k == ORCG_TYPE_TIMESTAMP_INSTANT) {
+        order.push_back({kSlotData, kInt});
+        order.push_back({kSlotSecondary, kInt});
+      } else if (k == ORCG_TYPE_LIST || k == ORCG_TYPE_MAP) {
+        order.push_back({kSlotLength, kInt});
+      }
+      bool ok = !order.empty();
+      for (auto& o : order) ok = ok && c.s[o.first].present && need_of[col * 5 + o.first] >= 0;
+      if (!ok) return;
+      const StreamInfo& ri = sf.streams[row_index[col]];
+      std::vector<uint8_t> ib;
+      std::vector<std::vector<uint64_t>> entries;
+      std::string e2;
+      if (!read_range(file, ri.offset, ri.length, ps.compression, ps.block_size, ib, e2) ||
+          !parse_row_index(ib.data(), ib.size(), entries) || entries.size() != G)
+        return;
+      // per stream: chunk header offsets (in the stream) -> decompressed starts
+      std::vector<std::vector<std::pair<uint64_t, uint64_t>>> cmap(order.size());
+      for (size_t o = 0; o < order.size(); ++o) {
+        const Need& nd = needs[need_of[col * 5 + order[o].first]];
+        uint64_t d = 0;
+        for (const Chunk& ch : nd.chunks) {
+          const uint64_t hdr = compressed ? ch.src_off - 3 - nd.file_off : ch.src_off - nd.file_off;
+          cmap[o].push_back({hdr, d});
+          d += ch.dst_len;
+        }
+        cmap[o].push_back({nd.file_off + 0, d});  // sentinel: the stream's end
+        cmap[o].back().first = ~0ull;
+      }
+      std::vector<std::vector<int64_t>> trips(order.size());
+      for (uint64_t g = 0; g < G && ok; ++g) {
+        const std::vector<uint64_t>& pv = entries[g];
+        size_t at = 0;
+        for (size_t o = 0; o < order.size() && ok; ++o) {
+          const size_t need_n = (compressed ? 2 : 1) + (order[o].second == kBool ? 2 : order[o].second == kRaw ? 0 : 1);
+          if (at + need_n > pv.size()) {
+            ok = false;
+            break;
+          }
+          uint64_t off;
+          const StreamBuf& sb = c.s[order[o].first];
+          if (compressed) {
+            const uint64_t chunk = pv[at], in = pv[at + 1];
+            auto& m = cmap[o];
+            auto it = std::lower_bound(m.begin(), m.end() - 1, std::make_pair(chunk, (uint64_t)0));
+            if (it != m.end() - 1 && it->first == chunk) off = it->second + in;
+            else if (it == m.end() - 1) off = m.back().second + in;  // position at the stream's end
+            else {
+              ok = false;
+              break;
+            }
+            at += 2;
+          } else {
+            off = pv[at++];
+          }
+          if (off > sb.len) {
+            ok = false;
+            break;
+          }
+          if (order[o].second != kRaw) {
+            const int64_t skip = (int64_t)pv[at++];
+            const int64_t bits = order[o].second == kBool ? (int64_t)pv[at++] : 0;
+            auto& t = trips[o];
+            if (!t.empty() && (uint64_t)t[t.size() - 3] > off) ok = false;
+            t.push_back((int64_t)off);
+            t.push_back(skip);
+            t.push_back(bits);
+          }
+        }
+      }
+      if (!ok) return;
+      for (size_t o = 0; o < order.size(); ++o) {
+        if (order[o].second == kRaw) continue;
+        StreamBuf& sb = c.s[order[o].first];
+        sb.pos = true;
+        sb.trip = std::move(trips[o]);
+      }
+      any = true;
+    });
+    if (any) hs.ngroups = G;
+  }
   // host run plans (header walks only) for every RLE stream, in parallel
   std::vector<StreamBuf*> rle;
   std::vector<int> rle_kind;  // 0 byte RLE, 1 RLEv1, 2 RLEv2
@@ -699,6 +886,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
       } else {
         kind = v1 ? 1 : 2;
       }
+      if (sb.pos) continue;  // cut by the row index
       rle.push_back(&sb);
       rle_kind.push_back(kind);
     }
@@ -710,6 +898,10 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     else if (rle_kind[q] == 1) sb.plan.reset(make_v1_plan(p, sb.len, 16u << 10, 8192));
     else sb.plan.reset(make_plan(p, sb.len, 16u << 10, 8192));
   });
+  hs.n_plan = rle.size();
+  hs.n_pos = 0;
+  for (auto& c : hs.cols)
+    for (auto& sb : c.s) hs.n_pos += sb.pos ? 1 : 0;
   uint64_t seg_bytes = 0;
   for (auto* sb : rle) seg_bytes += ((sb->plan->segs.size() * sizeof(orcg_segment)) + 255) & ~(uint64_t)255;
   w = (w + 255) & ~(uint64_t)255;
@@ -719,6 +911,24 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     const size_t nb = sb->plan->segs.size() * sizeof(orcg_segment);
     if (nb) memcpy(hs.h + w, sb->plan->segs.data(), nb);
     w = (w + nb + 255) & ~(uint64_t)255;
+  }
+  // row-index triplets and the row-group start rows
+  uint64_t rg_bytes = hs.ngroups ? ((hs.ngroups * 8 + 255) & ~(uint64_t)255) : 0;
+  for (auto& c : hs.cols)
+    for (auto& sb : c.s)
+      if (sb.pos) rg_bytes += ((sb.trip.size() * 8) + 255) & ~(uint64_t)255;
+  if (rg_bytes) {
+    if (!hs.ensure(w + rg_bytes + 64, w)) return hs.fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
+    hs.rows_off = w;
+    for (uint64_t g = 0; g < hs.ngroups; ++g) ((int64_t*)(hs.h + w))[g] = (int64_t)(g * footer.row_index_stride);
+    w = (w + hs.ngroups * 8 + 255) & ~(uint64_t)255;
+    for (auto& c : hs.cols)
+      for (auto& sb : c.s)
+        if (sb.pos) {
+          sb.rg_off = w;
+          memcpy(hs.h + w, sb.trip.data(), sb.trip.size() * 8);
+          w = (w + sb.trip.size() * 8 + 255) & ~(uint64_t)255;
+        }
   }
   hs.used = w;
   const double t2 = now_s();
@@ -742,7 +952,8 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   const double t1 = now_s();
   H = &hs;
   D = &ds;
-  rc = decode(0, footer.stripes[hs.stripe].num_rows, nullptr, footer.stripes[hs.stripe].num_rows);
+  rc = decode(0, footer.stripes[hs.stripe].num_rows, nullptr, footer.stripes[hs.stripe].num_rows,
+              hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr);
   if (!rc) {
     rc = sync_ctx(ctx);
     if (rc) rc = fail_ctx(rc);
@@ -779,6 +990,7 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
     return fail(ORCG_INVALID_ARGUMENT, "stripe index out of range");
   hipSetDevice(ctx->device);
   for (auto& t : timings) t = 0;
+  stream_stats[0] = stream_stats[1] = 0;
   while (slots.size() < count) slots.emplace_back(new DevSlot());
   nslots = 0;
   if (count == 0) return ORCG_OK;
@@ -786,6 +998,8 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   timings[0] += stages[0].t_parse;
   timings[1] += stages[0].t_decomp;
   timings[2] += stages[0].t_plan;
+  stream_stats[0] += stages[0].n_pos;
+  stream_stats[1] += stages[0].n_plan;
   if (rc) return fail(rc, stages[0].err);
   for (uint64_t k = 0; k < count; ++k) {
     HostStage& cur = stages[k & 1];
@@ -801,6 +1015,8 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
       timings[0] += nxt.t_parse;
       timings[1] += nxt.t_decomp;
       timings[2] += nxt.t_plan;
+      stream_stats[0] += nxt.n_pos;
+      stream_stats[1] += nxt.n_plan;
       if (nxt.rc) return fail(nxt.rc, nxt.err);
     }
   }
@@ -985,6 +1201,13 @@ int orcg_reader_copy_to_host(orcg_reader* r, void* dst, const void* src, uint64_
 int orcg_reader_last_timings(const orcg_reader* r, double* out5) {
   if (!r || !out5) return ORCG_INVALID_ARGUMENT;
   for (int i = 0; i < 5; ++i) out5[i] = r->timings[i];
+  return ORCG_OK;
+}
+
+int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2) {
+  if (!r || !out2) return ORCG_INVALID_ARGUMENT;
+  out2[0] = r->stream_stats[0];
+  out2[1] = r->stream_stats[1];
   return ORCG_OK;
 }
 

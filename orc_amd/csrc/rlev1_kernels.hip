@@ -152,6 +152,8 @@ __global__ __launch_bounds__(kWave) void rlev1_kernel(const uint8_t* __restrict_
     if (pos > seg_end) { if (lane == 0) report(err, vi, kErrBadSegment); return; }
   }
   if (lane == 0 && v_next != ~0ull && vi < value_end && vi != v_next) report(err, vi, kErrBadSegment);
+  // the last segment ran out of stream before the requested values
+  if (lane == 0 && v_next == ~0ull && vi < value_end) report(err, vi, kErrV1BadRead);
 }
 
 }  // namespace

@@ -126,6 +126,7 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
   if (vi >= value_end || v_next <= value_begin) return;  // no overlap with the output range
   if (seg_start >= seg_end) {
     if (v_next != ~0ull && v_next != vi && seg_start < src_len) report(err, vi, kErrBadSegment);
+    if (v_next == ~0ull) report(err, vi, kErrBadRead);  // no stream left for the requested values
     return;
   }
 
@@ -361,6 +362,7 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
     vi += L;
   }
   if (v_next != ~0ull && vi < value_end && vi != v_next) report(err, vi, kErrBadSegment);
+  if (v_next == ~0ull && vi < value_end) report(err, vi, kErrBadRead);  // stream ended early
 }
 
 }  // namespace

@@ -604,7 +604,28 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     const bool act = r < r1;
     const uint32_t hoff = act ? s_off[r] : s_off[c];
     const uint32_t val = act ? s_val[r] : 0u;
-    const Run run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
+    // the run's first 12 bytes in registers (one LDS round trip)
+    const uint32_t w0 = hoff >> 2, sh = hoff & 3u;
+    const uint32_t d0 = win[w0], d1 = win[w0 + 1], d2 = win[w0 + 2], d3 = win[w0 + 3];
+    const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh), b1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
+                   b2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    const uint32_t fb = b0 & 0xffu;
+    Run run;
+    if (__ballot(act && (fb >> 6) != 0) == 0) {
+      // SHORT_REPEAT only (low-cardinality streams): W + 1 value bytes, big endian
+      run.kind = 0;
+      run.L = (fb & 7u) + 3u;
+      const uint32_t nb = ((fb >> 3) & 7u) + 1u;
+      const uint64_t be = ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(b1, b0, 1)) << 32) |
+                          __builtin_bswap32(__builtin_amdgcn_alignbyte(b2, b1, 1));
+      const uint64_t v = be >> (64 - 8 * nb);
+      run.a = is_signed ? unzigzag(v) : v;
+      run.W = 8 * nb;
+      run.data = 1;
+      run.b = 0;
+    } else {
+      run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
+    }
     const bool shortr = act && run.kind != 2 && run.L <= kShortL;
     const uint32_t Ls = shortr ? run.L : 0u;
     const uint32_t incl = wave_scan_u32(Ls);
@@ -617,11 +638,15 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     }
     const bool mine = (uint32_t)lane < k;
     const uint32_t st0 = incl - Ls;
-    uint32_t maxl = mine ? Ls : 0u;
-    for (int m = 32; m >= 1; m >>= 1) maxl = max(maxl, (uint32_t)__shfl_xor((int)maxl, m));
-    uint64_t acc = 0;
-    for (uint32_t j = 0; j < maxl; ++j)
-      if (mine && j < Ls) stage[st0 + j] = short_value(win, run, hoff, j, is_signed, acc);
+    const uint32_t myl = mine ? Ls : 0u;
+    if (__ballot(mine && run.kind != 0) == 0) {
+      for (uint32_t j = 0; __ballot(j < myl) != 0; ++j)
+        if (j < myl) stage[st0 + j] = run.a;
+    } else {
+      uint64_t acc = 0;
+      for (uint32_t j = 0; __ballot(j < myl) != 0; ++j)
+        if (j < myl) stage[st0 + j] = short_value(win, run, hoff, j, is_signed, acc);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const uint32_t tot = rdlane(incl, k - 1);
@@ -706,6 +731,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   if (vi >= value_end || v_next <= value_begin) return;
   if (seg_start >= seg_end) {
     if (tid == 0 && v_next != ~0ull && v_next != vi && seg_start < src_len) report(err, vi, kErrBadSegment);
+    if (tid == 0 && v_next == ~0ull) report(err, vi, kErrBadRead);  // no stream left for the requested values
     return;
   }
 
@@ -877,6 +903,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     }
   }
   if (tid == 0 && v_next != ~0ull && vi < value_end && vi != v_next) report(err, vi, kErrBadSegment);
+  if (tid == 0 && v_next == ~0ull && vi < value_end) report(err, vi, kErrBadRead);  // stream ended early
 }
 
 }  // namespace

@@ -302,6 +302,12 @@ class Reader:
         return {"host_parse_s": t[0], "host_decompress_s": t[1], "host_plan_s": t[2], "h2d_s": t[3],
                 "device_decode_s": t[4]}
 
+    def last_stream_stats(self):
+        """RLE streams of the last read cut by the row index / by host plans."""
+        t = (ctypes.c_uint64 * 2)()
+        check(self._L.orcg_reader_last_stream_stats(self._h, t))
+        return {"row_index": t[0], "host_plan": t[1]}
+
     def read(self, fields=None):
         """All rows as dicts of the root struct's fields (pyarrow to_pylist shape)."""
         rows = []

@@ -10,6 +10,14 @@ if ROOT not in sys.path:
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# pyarrow (the file-level checker) resolves ORC writer zones under $TZDIR;
+# the image has no tzdata, so point it at the UTC zones of tests/tzdata.py
+if "TZDIR" not in os.environ:
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from tzdata import utc_tzdir
+
+    os.environ["TZDIR"] = utc_tzdir()
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")

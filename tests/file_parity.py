@@ -84,8 +84,27 @@ def pyarrow_rows(name, fields):
     return [] if t is None else t.to_pylist()
 
 
+def _ts_ns(x):
+    """Timestamps as int nanoseconds: pyarrow gives pandas Timestamps (or
+    datetimes), this reader numpy datetime64[ns]."""
+    import datetime
+
+    import numpy as np
+    if isinstance(x, np.datetime64):
+        return int(x.astype("datetime64[ns]").astype(np.int64))
+    if hasattr(x, "value") and hasattr(x, "nanosecond"):  # pandas.Timestamp
+        return int(x.value)
+    if isinstance(x, datetime.datetime):
+        d = x - datetime.datetime(1970, 1, 1, tzinfo=x.tzinfo)
+        return (d.days * 86400 + d.seconds) * 10 ** 9 + d.microseconds * 1000
+    return None
+
+
 def same(a, b):
     """Deep equality with NaN == NaN and float32-widened floats."""
+    ta, tb = _ts_ns(a), _ts_ns(b)
+    if ta is not None or tb is not None:
+        return ta == tb
     if isinstance(a, float) and isinstance(b, float):
         return (math.isnan(a) and math.isnan(b)) or a == b
     if isinstance(a, dict) and isinstance(b, dict):

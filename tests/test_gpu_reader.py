@@ -124,3 +124,36 @@ def test_pipelined_multi_stripe_read_matches_pyarrow(ctx, name):
             want = [None if x is None else (x - __import__("datetime").date(1970, 1, 1)).days for x in want]
         want = np.array([0 if x is None else x for x in want], dtype=np.int64)
         np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("name", ["demo-12-zlib.orc", "TestOrcFile.test1.orc", "nulls-at-end-snappy.orc",
+                                  "complextypes_iceberg.orc", "TestVectorOrcFile.testLz4.orc",
+                                  "orc-file-11-format.orc", "decimal.orc"])
+def test_row_index_segments_match_host_plans(ctx, name, monkeypatch):
+    """Streams cut at row groups by the ROW_INDEX positions (no host header
+    walk) decode exactly like the host-planned segmentation."""
+    r = orc_amd.Reader(path(name), ctx)
+    got = [r.read_stripe(s) for s in range(r.num_stripes)]
+    stats = r.last_stream_stats()
+    monkeypatch.setenv("ORCG_NO_ROW_INDEX", "1")
+    r2 = orc_amd.Reader(path(name), ctx)
+    want = [r2.read_stripe(s) for s in range(r2.num_stripes)]
+    assert r2.last_stream_stats()["row_index"] == 0
+    for a, b in zip(got, want):
+        assert set(a.columns) == set(b.columns)
+        for tid in a.columns:
+            ca, cb = a.columns[tid], b.columns[tid]
+            for f in ("not_null", "data", "length", "offsets", "secondary"):
+                x, y = getattr(ca, f), getattr(cb, f)
+                assert (x is None) == (y is None), (tid, f)
+                if x is not None:
+                    assert np.array_equal(x, y), (name, tid, f)
+    if r.row_index_stride and r.num_rows:
+        assert stats["row_index"] > 0, stats
+
+
+def test_file_without_row_index_uses_host_plans(ctx):
+    r = orc_amd.Reader(path("TestOrcFile.testWithoutIndex.orc"), ctx)
+    r.read_stripe(0)
+    st = r.last_stream_stats()
+    assert st["row_index"] == 0 and st["host_plan"] > 0
