@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <functional>
 #include <chrono>
 #include <cstring>
 #include <map>
@@ -253,9 +254,25 @@ struct orcg_reader {
   double timings[5] = {0, 0, 0, 0, 0};
   uint64_t stream_stats[2] = {0, 0};  // last read: RLE streams cut by the row index, by host plans
 
+  // Checks whose operands are device scalars (dictionary blob size, varint
+  // counts, string bytes): their D2H copies are queued on the stream and the
+  // checks run, in column order, after the stripe's one synchronisation
+  // instead of a synchronisation each. The reference makes them inline.
+  uint64_t* h_defer = nullptr;
+  size_t defer_cap = 0, defer_used = 0;
+  std::vector<std::function<int()>> checks;
+  const uint64_t* defer(const void* d_src, size_t count) {
+    if (defer_used + count > defer_cap) return nullptr;
+    uint64_t* h = h_defer + defer_used;
+    defer_used += count;
+    if (hipMemcpyAsync(h, d_src, count * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) return nullptr;
+    return h;
+  }
+
   ~orcg_reader() {
     slots.clear();
     if (mapped) munmap(mapped, file_len);
+    if (h_defer) (void)hipHostFree(h_defer);
   }
   int fail(int status, const std::string& m) {
     last_error = m;
@@ -491,15 +508,15 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       ORCG_ALLOC(int64_t, base, sb.len / 16384 + 3);
       if ((rc = launch_varint_tile_counts(ctx, d_src, sb.len, counts, &ntiles))) return fail_ctx(rc);
       if ((rc = launch_exclusive_scan(ctx, counts, ntiles, base))) return fail_ctx(rc);
-      uint64_t total = 0;
-      if ((rc = hip_check(ctx, hipMemcpyAsync(&total, base + ntiles, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
-          (rc = sync_ctx(ctx)))
-        return fail_ctx(rc);
-      if (total < nonnull)
-        return fail(ORCG_PARSE_ERROR, "Read past end of stream in Decimal64ColumnReader column " + cid + " kind DATA");
+      const uint64_t* total = defer(base + ntiles, 1);
+      if (!total) return fail(ORCG_DEVICE_ERROR, "D2H of the varint count failed");
+      checks.push_back([this, total, nonnull, cid]() -> int {
+        return *total < nonnull ? fail(ORCG_PARSE_ERROR, "Read past end of stream in Decimal64ColumnReader column " +
+                                                             cid + " kind DATA")
+                                : ORCG_OK;
+      });
       ORCG_ALLOC(int64_t, dense, wide ? 2 * nonnull : nonnull);
-      if ((rc = launch_varint_decimal(ctx, d_src, sb.len, base, scales, nonnull, (int32_t)t.scale, wide, dense)) ||
-          (rc = sync_ctx(ctx)))
+      if ((rc = launch_varint_decimal(ctx, d_src, sb.len, base, scales, nonnull, (int32_t)t.scale, wide, dense)))
         return fail_ctx(rc);
       if (!row_nn) {
         c.data = dense;
@@ -571,18 +588,22 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
       if ((rc = hip_check(ctx, hipMemcpyAsync(D->d_scalars, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream), "copy")))
         return fail_ctx(rc);
-      uint64_t h[2] = {0, 0};  // blob bytes, negative-length flag
-      if ((rc = hip_check(ctx, hipMemcpyAsync(h, D->d_scalars, 16, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
-          (rc = sync_ctx(ctx)))
-        return fail_ctx(rc);
-      if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
+      const uint64_t* h = defer(D->d_scalars, 2);  // blob bytes, negative-length flag
+      if (!h) return fail(ORCG_DEVICE_ERROR, "D2H of the dictionary size failed");
       StreamBuf& db = c.s[kSlotDict];
-      if (h[0] > 0 && !db.present)
-        return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
-      if (h[0] > (db.present ? db.len : 0)) return fail(ORCG_PARSE_ERROR, "bad read in readFully");
+      Col* cp = &c;
+      const bool db_present = db.present;
+      const uint64_t db_len = db.present ? db.len : 0;
+      checks.push_back([this, h, cp, db_present, db_len, cid]() -> int {
+        if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
+        if (h[0] > 0 && !db_present)
+          return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
+        if (h[0] > db_len) return fail(ORCG_PARSE_ERROR, "bad read in readFully");
+        cp->blob_len = h[0];
+        return ORCG_OK;
+      });
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDictionaryColumn");
       c.blob = db.present ? D->d_stage + db.host_off : nullptr;
-      c.blob_len = h[0];
       ORCG_ALLOC(int64_t, idx, nonnull);
       if ((rc = int_stream(c, kSlotData, false, nonnull, idx))) return rc;
       int64_t* ridx = idx;
@@ -603,11 +624,12 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       StreamBuf& db = c.s[kSlotData];
       c.blob = D->d_stage + db.host_off;
       c.blob_len = db.len;
-      uint64_t need = 0;
-      if ((rc = hip_check(ctx, hipMemcpyAsync(&need, dstart + nonnull, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
-          (rc = sync_ctx(ctx)))
-        return fail_ctx(rc);
-      if (need > c.blob_len) return fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next");
+      const uint64_t* need = defer(dstart + nonnull, 1);
+      if (!need) return fail(ORCG_DEVICE_ERROR, "D2H of the string bytes failed");
+      const uint64_t blob_len = c.blob_len;
+      checks.push_back([this, need, blob_len]() -> int {
+        return *need > blob_len ? fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next") : ORCG_OK;
+      });
       if (row_nn) {
         if ((rc = scatter(dstart, row_nn, n, start, 8))) return fail_ctx(rc);
         if ((rc = scatter(dlen, row_nn, n, len, 8))) return fail_ctx(rc);
@@ -952,12 +974,32 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   const double t1 = now_s();
   H = &hs;
   D = &ds;
+  const size_t need_defer = 4 * hs.cols.size() + 16;
+  if (defer_cap < need_defer) {
+    if (h_defer) (void)hipHostFree(h_defer);
+    h_defer = nullptr;
+    defer_cap = 0;
+    if (hipHostMalloc((void**)&h_defer, need_defer * 8, hipHostMallocDefault) != hipSuccess)
+      return fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed");
+    defer_cap = need_defer;
+  }
+  defer_used = 0;
+  checks.clear();
   rc = decode(0, footer.stripes[hs.stripe].num_rows, nullptr, footer.stripes[hs.stripe].num_rows,
               hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr);
+  if (rc) (void)hipStreamSynchronize(ctx->stream);  // queued copies land before the buffer is reused
   if (!rc) {
-    rc = sync_ctx(ctx);
-    if (rc) rc = fail_ctx(rc);
+    // the checks first (in column order, as the reference raises them), then
+    // the device error record
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) rc = fail(ORCG_DEVICE_ERROR, "stream synchronize failed");
+    for (auto& ch : checks)
+      if (!rc) rc = ch();
+    if (!rc) {
+      rc = sync_ctx(ctx);
+      if (rc) rc = fail_ctx(rc);
+    }
   }
+  checks.clear();
   ds.out.assign(hs.cols.size(), ColOut());
   for (size_t i = 0; i < hs.cols.size(); ++i) {
     const Col& c = hs.cols[i];

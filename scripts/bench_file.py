@@ -1,15 +1,24 @@
 #!/usr/bin/env python3
-"""File-path benchmark (BASELINE.json configs[2], "C3"): the demo-12-zlib
-schema at 10^8 synthetic rows, zlib, 64 MB stripes. Host zlib decompression
--> one H2D per stripe -> GPU decode of every column (RLEv2 ints, dictionary
-strings), timed per phase, next to pyarrow's ORC C++ reader (1 thread) on the
-same file.
+"""File-path benchmarks (BASELINE.json configs[2..4]): ORC file bytes in host
+memory -> host block decompression + stripe / row-index parse -> one H2D per
+stripe -> GPU decode of every column into HBM (stripe i+1 prepared on the
+host while stripe i decodes), next to pyarrow's ORC C++ reader (1 thread) on
+the same file.
 
-The file is built from tests/golden/files/demo-12-zlib.orc by tiling its
-1,920,800 rows 52x (_col0 offset per tile so it stays a row id) and writing
-it with pyarrow (ORC C++ writer), dictionary encoding enabled.
+Workloads (--workload):
+  c3  demo-12-zlib schema at ~10^8 rows: the example's 1,920,800 rows tiled
+      52x (_col0 offset per tile), zlib, 64 MB stripes, dictionary strings.
+  c4  TPC-H lineitem-like, 16 columns (sorted orderkey with 1-7 repeats,
+      uniform part/suppkey, linenumber, 4 decimal(15,2), 3 dates, 4
+      low-cardinality dictionary strings, direct comment strings), zstd.
+  c5  struct<a:list<int>, m:map<string,int>> with 10 % nulls at every level,
+      list / map lengths U[0, 8], 16 map keys, zstd.
 
-    python scripts/bench_file.py [--rows 99881600] [--iters 3]
+Multi-GPU: under torch.distributed.run each rank decodes a contiguous stripe
+range (RowReaderOptions::range; orc_amd.shard.partition_stripes) with no
+collective in the timed region; value = all rows / max-over-ranks time.
+
+    python scripts/bench_file.py --workload c4 [--rows 10000000] [--iters 3]
 """
 import argparse
 import json
@@ -24,7 +33,7 @@ sys.path.insert(0, ROOT)
 DEMO12 = os.path.join(ROOT, "tests", "golden", "files", "demo-12-zlib.orc")
 
 
-def make_file(path, rows, stripe_mb):
+def make_c3(path, rows, stripe_mb):
     import pyarrow as pa
     import pyarrow.compute as pc
     import pyarrow.orc as po
@@ -44,110 +53,247 @@ def make_file(path, rows, stripe_mb):
     table = pa.concat_tables(parts)
     po.write_table(table, path, compression="zlib", stripe_size=stripe_mb << 20,
                    dictionary_key_size_threshold=1.0, row_index_stride=10000)
-    return table.num_rows
 
 
-def output_bytes(reader):
-    """Decoded bytes per row of the batch layout (int64 per int column,
-    start + length per string column)."""
-    per_row = 0
-    for st in reader.types[0].subtypes:
-        k = reader.types[st].kind
-        per_row += 16 if k in (7, 8, 16, 17) else 8
-    return per_row
+def _decimal(pa, cents, precision, scale):
+    """decimal128(precision, scale) array of the int64 unscaled values."""
+    v = np.ascontiguousarray(cents, dtype=np.int64)
+    buf = np.empty((v.size, 2), dtype=np.int64)
+    buf[:, 0] = v
+    buf[:, 1] = v >> 63
+    return pa.Array.from_buffers(pa.decimal128(precision, scale), v.size, [None, pa.py_buffer(buf.tobytes())])
+
+
+def _dict_strings(pa, rng, words, n):
+    idx = pa.array(rng.integers(0, len(words), size=n).astype(np.int32))
+    return pa.DictionaryArray.from_arrays(idx, pa.array(words)).cast(pa.string())
+
+
+def make_c4(path, rows, stripe_mb):
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    import pyarrow.orc as po
+
+    rng = np.random.default_rng(4)
+    reps = rng.integers(1, 8, size=rows // 2 + 8)
+    reps = reps[: np.searchsorted(np.cumsum(reps), rows) + 1]
+    okey = np.repeat(np.arange(1, reps.size + 1, dtype=np.int64) * 4, reps)[:rows]
+    line = (np.arange(okey.size) - np.repeat(np.cumsum(reps) - reps, reps)[:rows] + 1).astype(np.int32)
+    qty = rng.integers(1, 51, size=rows)
+    price = qty * rng.integers(90_000, 210_000, size=rows) // 100
+    ship = rng.integers(8036, 10561, size=rows).astype(np.int32)  # 1992-01-02 .. 1998-12-01
+    pool = pa.array(["".join(chr(97 + c) for c in rng.integers(0, 26, size=int(rng.integers(5, 22))))
+                     for _ in range(4096)])
+    c1 = pc.take(pool, pa.array(rng.integers(0, 4096, size=rows)))
+    c2 = pc.take(pool, pa.array(rng.integers(0, 4096, size=rows)))
+    table = pa.table({
+        "l_orderkey": pa.array(okey),
+        "l_partkey": pa.array(rng.integers(1, 20_000_001, size=rows)),
+        "l_suppkey": pa.array(rng.integers(1, 1_000_001, size=rows)),
+        "l_linenumber": pa.array(line),
+        "l_quantity": _decimal(pa, qty * 100, 15, 2),
+        "l_extendedprice": _decimal(pa, price, 15, 2),
+        "l_discount": _decimal(pa, rng.integers(0, 11, size=rows), 15, 2),
+        "l_tax": _decimal(pa, rng.integers(0, 9, size=rows), 15, 2),
+        "l_returnflag": _dict_strings(pa, rng, ["A", "N", "R"], rows),
+        "l_linestatus": _dict_strings(pa, rng, ["O", "F"], rows),
+        "l_shipdate": pa.array(ship, type=pa.date32()),
+        "l_commitdate": pa.array(ship + rng.integers(-60, 60, size=rows).astype(np.int32), type=pa.date32()),
+        "l_receiptdate": pa.array(ship + rng.integers(1, 31, size=rows).astype(np.int32), type=pa.date32()),
+        "l_shipinstruct": _dict_strings(pa, rng, ["DELIVER IN PERSON", "COLLECT COD", "NONE",
+                                                  "TAKE BACK RETURN"], rows),
+        "l_shipmode": _dict_strings(pa, rng, ["REG AIR", "AIR", "RAIL", "SHIP", "TRUCK", "MAIL", "FOB"], rows),
+        "l_comment": pc.binary_join_element_wise(c1, c2, " "),
+    })
+    po.write_table(table, path, compression="zstd", stripe_size=stripe_mb << 20,
+                   dictionary_key_size_threshold=0.5, row_index_stride=10000)
+
+
+def make_c5(path, rows, stripe_mb):
+    import pyarrow as pa
+    import pyarrow.orc as po
+
+    rng = np.random.default_rng(5)
+
+    def lengths(n):
+        ln = rng.integers(0, 9, size=n)
+        null = rng.random(n) < 0.1
+        ln[null] = 0
+        off = np.concatenate([[0], np.cumsum(ln)]).astype(np.int32)
+        return off, null
+
+    off_a, null_a = lengths(rows)
+    na = int(off_a[-1])
+    vals = pa.array(rng.integers(-(1 << 31), 1 << 31, size=na).astype(np.int32), mask=rng.random(na) < 0.1)
+    a = pa.ListArray.from_arrays(pa.array(off_a), vals, mask=pa.array(null_a))
+    off_m, null_m = lengths(rows)
+    nm = int(off_m[-1])
+    keys = pa.DictionaryArray.from_arrays(pa.array(rng.integers(0, 16, size=nm).astype(np.int32)),
+                                          pa.array(["key%02d" % i for i in range(16)])).cast(pa.string())
+    items = pa.array(rng.integers(0, 1 << 20, size=nm).astype(np.int32), mask=rng.random(nm) < 0.1)
+    m = pa.MapArray.from_arrays(pa.array(off_m), keys, items, mask=pa.array(null_m))
+    s = pa.StructArray.from_arrays([a, m], names=["a", "m"], mask=pa.array(rng.random(rows) < 0.1))
+    po.write_table(pa.table({"s": s}), path, compression="zstd", stripe_size=stripe_mb << 20,
+                   dictionary_key_size_threshold=1.0, row_index_stride=10000)
+
+
+WORKLOADS = {
+    "c3": (make_c3, 52 * 1920800, "configs[2]: demo-12-zlib schema at %d rows, zlib, %d MB stripes"),
+    "c4": (make_c4, 10_000_000, "configs[3] (one GPU's share): TPC-H lineitem-like 16 columns at %d rows, zstd, "
+                                "%d MB stripes"),
+    "c5": (make_c5, 10_000_000, "configs[4] (one GPU's share): struct<list<int>, map<string,int>> with 10%% nulls "
+                                "at %d rows, zstd, %d MB stripes"),
+}
+
+
+def view_bytes(v, kind, precision):
+    """Device bytes of one decoded column view (the batch layout of
+    include/orcg_reader.h)."""
+    n = v.num_elements
+    b = n if v.has_nulls else 0
+    if kind in (7, 8, 16, 17):  # strings: start + length
+        b += 16 * n
+    elif kind in (10, 11):  # list / map offsets
+        b += 8 * (n + 1)
+    elif kind == 14:
+        b += (16 if precision > 18 else 8) * n
+    elif kind in (9, 18):
+        b += 16 * n
+    elif kind != 12:
+        b += 8 * n
+    return b
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rows", type=int, default=52 * 1920800)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--stripe-mb", type=int, default=64)
     ap.add_argument("--path", default=None)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-copy", action="store_true", help="also time decode + D2H into host batches")
     args = ap.parse_args()
-    path = args.path or "/tmp/orcg_c3_%d.orc" % args.rows
+    maker, default_rows, desc = WORKLOADS[args.workload]
+    rows = args.rows or default_rows
+    path = args.path or "/tmp/orcg_%s_%d.orc" % (args.workload, rows)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     t0 = time.time()
-    if not os.path.exists(path):
-        make_file(path, args.rows, args.stripe_mb)
+    if rank == 0 and not os.path.exists(path):
+        maker(path + ".tmp", rows, args.stripe_mb)
+        os.replace(path + ".tmp", path)
     t_make = time.time() - t0
 
-    import torch  # noqa: F401
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.barrier()  # the file exists
 
     import orc_amd
+    from orc_amd.shard import reader_ranges
 
-    ctx = orc_amd.Context(0)
+    ctx = orc_amd.Context(local_rank)
     r = orc_amd.Reader(path, ctx)
     nrows = r.num_rows
     fsize = os.path.getsize(path)
-    per_row = output_bytes(r)
+    ranges, stripe_rows = reader_ranges(r, world)
+    first, last = ranges[rank]
+    my_rows = int(sum(stripe_rows[first:last]))
 
     def full_pass():
-        # every stripe decoded into HBM, host prepare of stripe i+1 overlapped
-        # with the GPU decode of stripe i
         t = time.perf_counter()
-        r.read_stripes_device()
+        if last > first:
+            r.read_stripes_device(first, last - first)
         wall = time.perf_counter() - t
         tm = r.last_timings()
         return wall, np.array([tm["host_parse_s"], tm["host_decompress_s"], tm["host_plan_s"], tm["h2d_s"],
                                tm["device_decode_s"]])
 
-    def serial_pass():
-        t = time.perf_counter()
-        for s in range(r.num_stripes):
-            r.read_stripe_device(s)
-        return time.perf_counter() - t
-
     full_pass()  # warm-up (allocations, page cache)
+    if dist:
+        dist.barrier()
     runs = [full_pass() for _ in range(args.iters)]
-    best = min(runs, key=lambda x: x[0])
-    wall, ph = best
-    serial = min(serial_pass() for _ in range(args.iters))
+    wall, ph = min(runs, key=lambda x: x[0])
+    if dist:
+        t = torch.tensor([wall], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    stats = r.last_stream_stats()
 
-    # correctness spot check against pyarrow on the first stripe
-    import pyarrow.orc as po
-    b = r.read_stripe(0)
-    got = b.to_pylist(["_col0", "_col3", "_col4"])[:50000]
-    want = po.ORCFile(path).read_stripe(0, columns=["_col0", "_col3", "_col4"]).to_pylist()[:50000]
-    if got != want:
-        raise SystemExit("C3 decode mismatch against pyarrow")
+    # decoded bytes (device batch layout) of this rank's stripes
+    dec_bytes = 0
+    for k in range(last - first):
+        for t in r.types:
+            v = r.stripe_column_view(k, t.id)
+            if v.decoded:
+                dec_bytes += view_bytes(v, t.kind, t.precision)
+
+    check = None
+    if rank == 0 and r.num_stripes:
+        # correctness spot check: stripe 0 against pyarrow (the reference C++ reader)
+        import pyarrow.orc as po
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from file_parity import first_difference
+
+        got = r.read_stripe(0).to_pylist()
+        want = po.ORCFile(path).read_stripe(0).to_pylist()
+        diff = first_difference(want, got)
+        if diff:
+            raise SystemExit("%s decode mismatch against pyarrow: %s" % (args.workload, diff))
+        check = "stripe 0 (%d rows) equal to pyarrow" % len(got)
 
     host = None
-    if args.host_copy:
+    if args.host_copy and rank == 0:
         t = time.perf_counter()
-        for s in range(r.num_stripes):
+        for s in range(first, last):
             r.read_stripe(s)
         host = time.perf_counter() - t
 
     cpu = None
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and rank == 0:
         import pyarrow as pa
+        import pyarrow.orc as po
         pa.set_cpu_count(1)
         t = time.perf_counter()
         po.ORCFile(path).read()
         tc = time.perf_counter() - t
         cpu = {"value": round(nrows / tc / 1e6, 2), "unit": "Mrows/s", "cores": 1, "kind": "reference",
-               "sample": "pyarrow %s (ORC C++ reader) full read of the same file, 1 thread, %.2f s" % (pa.__version__, tc)}
+               "sample": "pyarrow %s (ORC C++ reader) full read of the same file to Arrow, 1 thread, %.2f s"
+                         % (pa.__version__, tc)}
 
-    line = {
-        "metric": "file decode Mrows/s, demo-12 schema, host zlib -> H2D -> GPU decode",
-        "config": {"workload": "configs[2]: demo-12-zlib schema at %d rows, zlib, %d MB stripes" % (nrows, args.stripe_mb),
-                   "stripes": r.num_stripes, "file_bytes": fsize, "decoded_bytes_per_row": per_row,
-                   "host_threads": int(os.environ.get("ORCG_HOST_THREADS", "0")) or min(16, os.cpu_count() or 1)},
-        "value": round(nrows / wall / 1e6, 2),
-        "unit": "Mrows/s",
-        "decoded_GBps": round(nrows * per_row / wall / 1e9, 2),
-        "wall_s": round(wall, 4),
-        "serial_wall_s": round(serial, 4),
-        "phases_s_summed_over_stripes": {"host_parse": round(ph[0], 4), "host_decompress": round(ph[1], 4),
-                                         "host_plan": round(ph[2], 4), "h2d": round(ph[3], 4),
-                                         "device_decode": round(ph[4], 4)},
-        "device_decode_Mrows_per_s": round(nrows / ph[4] / 1e6, 1),
-        "host_batch_copy_s": None if host is None else round(host, 3),
-        "cpu_baseline": cpu,
-        "make_file_s": round(t_make, 1),
-    }
-    print(json.dumps(line), flush=True)
+    if rank == 0:
+        line = {
+            "metric": "file decode Mrows/s (host decompress -> H2D -> GPU decode into HBM)",
+            "workload": args.workload,
+            "config": {"workload": desc % (nrows, args.stripe_mb), "stripes": r.num_stripes, "file_bytes": fsize,
+                       "n_gpus": world, "host_threads": int(os.environ.get("ORCG_HOST_THREADS", "0"))
+                       or min(16, os.cpu_count() or 1)},
+            "value": round(nrows / wall / 1e6, 2),
+            "unit": "Mrows/s",
+            "decoded_GBps": round(dec_bytes * world / wall / 1e9, 2),
+            "decoded_bytes_per_row": round(dec_bytes / max(my_rows, 1), 1),
+            "wall_s": round(wall, 4),
+            "phases_s_summed_over_stripes": {"host_parse": round(ph[0], 4), "host_decompress": round(ph[1], 4),
+                                             "host_plan_and_row_index": round(ph[2], 4), "h2d": round(ph[3], 4),
+                                             "device_decode": round(ph[4], 4)},
+            "device_decode_Mrows_per_s": round(my_rows / max(ph[4], 1e-9) / 1e6, 1),
+            "rle_streams": stats,
+            "host_batch_copy_s": None if host is None else round(host, 3),
+            "check": check,
+            "cpu_baseline": cpu,
+            "make_file_s": round(t_make, 1),
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
