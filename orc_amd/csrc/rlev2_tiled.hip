@@ -312,6 +312,76 @@ struct WalkResult {
   uint32_t n, stop, dpos, dval;
 };
 
+// terminator bits of a dword's bytes (bit i = byte i < 0x80)
+__device__ __forceinline__ uint32_t term4(uint32_t w) {
+  const uint32_t m = (~w >> 7) & 0x01010101u;
+  return (m * 0x10204080u) >> 28;
+}
+
+// The serial walk's view of a run: bytes, values and the error parse_run
+// would report, in its order. SHORT_REPEAT / DIRECT from the first two
+// bytes, DELTA from a terminator mask of the 24 bytes after its header
+// (two varints of <= 11 bytes: every writer's); PATCHED_BASE and longer
+// varints through parse_run.
+__device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint64_t avail, int is_signed,
+                                            uint32_t* bytes, uint32_t* L, uint32_t* err) {
+  const uint32_t fb = hw.byte(lp), kind = fb >> 6;
+  *err = kErrNone;
+  if (kind == 0) {
+    *bytes = 2u + ((fb >> 3) & 7u);
+    *L = (fb & 7u) + 3u;
+    if (*bytes > avail) *err = kErrBadRead;
+    return;
+  }
+  if (kind != 2) {
+    if (avail < 2) {
+      *err = kErrBadRead;
+      *bytes = 0;
+      *L = 0;
+      return;
+    }
+    const uint32_t L2 = ((fb & 1u) << 8 | hw.byte(lp + 1)) + 1u;
+    const uint32_t code = (fb >> 1) & 0x1fu;
+    if (kind == 1) {
+      *L = L2;
+      *bytes = 2u + (fbs_width(code) * L2 + 7u) / 8u;
+      if (*bytes > avail) *err = kErrBadRead;
+      return;
+    }
+    // DELTA: varint lengths from the terminator mask of bytes lp+2 .. lp+25
+    const uint32_t o = lp + 2u - hw.base, i0 = o >> 2, sh = o & 3u;
+    uint32_t t = 0, prev = rdlane(hw.word, i0);
+#pragma unroll
+    for (uint32_t k = 0; k < 6; ++k) {
+      const uint32_t nx = rdlane(hw.word, i0 + k + 1);
+      t |= term4(__builtin_amdgcn_alignbyte(nx, prev, sh)) << (4 * k);
+      prev = nx;
+    }
+    const uint32_t n1 = t ? (uint32_t)__builtin_ctz(t) + 1u : 32u;
+    const uint32_t t2 = n1 < 24 ? t >> n1 : 0u;
+    const uint32_t n2 = t2 ? (uint32_t)__builtin_ctz(t2) + 1u : 32u;
+    if (n1 <= 11 && n2 <= 11) {
+      const uint32_t W = code ? fbs_width(code) : 0u;
+      *L = L2;
+      if (2u + n1 + n2 > avail) {
+        *err = kErrBadRead;
+        return;
+      }
+      if (W != 0 && L2 < 2) {
+        *err = kErrDeltaLength;
+        return;
+      }
+      *bytes = 2u + n1 + n2 + (W ? (W * (L2 - 2u) + 7u) / 8u : 0u);
+      if (*bytes > avail) *err = kErrBadRead;
+      return;
+    }
+  }
+  const Run r = parse_run([&](uint32_t i) { return hw.byte(lp + i); }, avail, kHdrLim, is_signed);
+  *bytes = r.bytes;
+  *L = r.L;
+  *err = r.err;
+}
+
 // Wave-uniform header walk over the window [wpos, wpos + kWin): records runs
 // starting at pos.. into (run_off, run_val) until the next run starts past
 // kWin - kMaxRun, leaves the segment, or the table is full.
@@ -329,10 +399,10 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
     const uint32_t lp = (uint32_t)(p - wpos);
     if (lp >= kChunk && n > 0) break;  // starts in the next window
     hw.cover(win, lp, kWin / 4 + 8, lane);
-    const Run r = parse_run([&](uint32_t i) { return hw.byte(lp + i); }, src_len - p, kHdrLim, is_signed);
-    uint32_t e = r.err;
-    if (e == kErrNone && p + r.bytes > seg_end) e = kErrBadSegment;
-    if (e == kErrNone && lp + r.bytes > lim) e = kErrBadRead;  // only a corrupt varint gets here
+    uint32_t rbytes, rL, e;
+    walk_extent(hw, lp, src_len - p, is_signed, &rbytes, &rL, &e);
+    if (e == kErrNone && p + rbytes > seg_end) e = kErrBadSegment;
+    if (e == kErrNone && lp + rbytes > lim) e = kErrBadRead;  // only a corrupt varint gets here
     if (e != kErrNone) {
       if (lane == 0) report(err, v, e);
       stop = 1;
@@ -343,8 +413,8 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
       run_val[n] = (uint32_t)(v - vi);
     }
     ++n;
-    p += r.bytes;
-    v += r.L;
+    p += rbytes;
+    v += rL;
   }
   return WalkResult{n, stop, (uint32_t)(p - pos), (uint32_t)(v - vi)};
 }
@@ -945,6 +1015,8 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
     case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
     case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 4, true); break;  // dense-capable, 21 KB
     case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true); break;  // dense-capable, 13 KB
+    case 12: ORCG_KT(kOptNTStore | kOptFast, 21, true, 3, false); break;               // producer wave, 2 x 21 KB
+    case 13: ORCG_KT(kOptNTStore | kOptFast, 13, true, 4, false); break;               // producer wave, 2 x 13 KB
     default: {
       // ORCG_RLEV2_TILED picks the instance by stream density: wide values
       // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
