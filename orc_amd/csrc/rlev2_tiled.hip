@@ -258,6 +258,31 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
   const uint64_t v1 = r.a + r.b;
   const bool neg = (int64_t)r.b < 0;
   uint64_t carry = 0;  // wave-uniform running |delta| total
+  if (W <= 26 && (kOpt & kOptFast) && L == 512 && v0 >= value_begin && v0 + 512 <= value_end) {
+    // full run inside the output range: all 8 chunks' deltas loaded up
+    // front, no per-value predicates, one 32-bit wave scan per chunk
+    T* out = dst + (v0 - value_begin);
+    uint32_t dl[kMaxRunUnroll];
+#pragma unroll
+    for (int it = 0; it < kMaxRunUnroll; ++it) {
+      const uint32_t j = it * kWave + lane;
+      const uint32_t k = j >= 2 ? j - 2 : 0u;  // j < 2: a dummy in-range read, masked below
+      const uint32_t bit = k * W;
+      const uint32_t br = d + (bit >> 3);
+      dl[it] = (uint32_t)field(lds12(win, br), br, bit & 7u, W);
+    }
+    if (lane < 2) dl[0] = 0;
+#pragma unroll
+    for (int it = 0; it < kMaxRunUnroll; ++it) {
+      const uint32_t j = it * kWave + lane;
+      const uint32_t s32 = wave_scan_u32(dl[it]);
+      const uint64_t sum = carry + s32;
+      carry += (uint32_t)__builtin_amdgcn_readlane((int)s32, 63);
+      const uint64_t v = j == 0 ? r.a : (j == 1 ? v1 : (neg ? v1 - sum : v1 + sum));
+      store1<kOpt>(out + j, v);
+    }
+    return;
+  }
   if (W <= 26) {
     // 64 deltas of <= 26 bits sum below 2^32: scan in 32 bits
 #pragma unroll 1
