@@ -70,6 +70,7 @@ constexpr uint32_t kShortL = 16;             // runs of <= kShortL values go lan
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kDpErr = 0x80000000u;     // DP entry: a corrupt run starts here
 constexpr uint16_t kSink = 0xffffu;          // chain successor: none
+constexpr uint32_t kWalkDone = 0x80000000u;  // published-runs flag: the walk has finished
 // density hysteresis (stream bytes per run of the last pass)
 constexpr uint32_t kToDense = 24, kToSerial = 64;
 
@@ -415,7 +416,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
                                            uint64_t wpos, uint64_t pos, uint64_t vi, uint64_t seg_end,
                                            uint64_t src_len, uint64_t value_end, int is_signed,
                                            unsigned long long* err, int lane, uint32_t lim = kWin,
-                                           uint32_t cap = kCap) {
+                                           uint32_t cap = kCap, uint32_t* pub = nullptr) {
   constexpr uint32_t kChunk = kWin - kMaxRun;
   uint64_t p = pos, v = vi;
   uint32_t n = 0, stop = 0;
@@ -436,6 +437,8 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
     if (lane == 0) {
       run_off[n] = lp;
       run_val[n] = (uint32_t)(v - vi);
+      // expanding waves may claim the run as soon as it is published
+      if (pub) __hip_atomic_store(pub, n + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     ++n;
     p += rbytes;
@@ -801,6 +804,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   __shared__ uint32_t s_win[kBufs][kWin / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
   __shared__ uint32_t s_tab[kBufs][2 * kCap];
   __shared__ uint32_t s_ctl[kBufs][12];
+  __shared__ uint32_t s_sync[2][2];  // serial passes: {published runs, claimed runs}, by pass parity
   __shared__ DenseLds<kDense> s_dense;
   uint32_t* s_off[kBufs];
   uint32_t* s_val[kBufs];
@@ -840,6 +844,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   const uint64_t bias = (uint64_t)(base_abs - (uintptr_t)src);  // stream offset of descriptor byte 0
 
   uint64_t pos = seg_start;
+  uint32_t sync_par = 0;
+  if (tid < 4) s_sync[tid >> 1][tid & 1] = 0;  // ordered before use by the first window's barrier
   PROF_DECL;
   if constexpr (!kPipe) {
     uint64_t pwpos = ~0ull;  // previous window (stream offset) and its valid bytes
@@ -904,33 +910,54 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
                                value_begin, value_end, dst, lane);
           }
         } else {
+          // Wave 0 walks and publishes each run as it is found; every wave
+          // (wave 0 once its walk is done) claims published runs from an LDS
+          // counter and expands them, so the walk overlaps the expansion.
+          uint32_t* s_pub = &s_sync[sync_par][0];
+          uint32_t* s_claim = &s_sync[sync_par][1];
           if (wave == 0) {
-            // the walk is the workgroup's critical path (the other waves wait
-            // at the barrier): raise its issue priority over co-resident
-            // waves that are expanding
+            // the walk is the workgroup's critical path: raise its issue
+            // priority over co-resident waves that are expanding
             __builtin_amdgcn_s_setprio(3);
             // dense instances: a short first walk (the probe) measures the
             // stream's bytes per run before committing to a mode
             const uint32_t cap = (kDense && probe) ? 32u : kCap;
             const WalkResult w = walk<kWin, kCap>(s_win[0], s_off[0], s_val[0], wpos, pos, vi, seg_end, src_len,
-                                                  value_end, is_signed, err, lane, need, cap);
+                                                  value_end, is_signed, err, lane, need, cap, s_pub);
             if (lane == 0) {
               s_ctl[0][0] = w.n;
               s_ctl[0][1] = w.stop;
               s_ctl[0][2] = w.dpos;
               s_ctl[0][3] = w.dval;
+              __hip_atomic_store(s_pub, w.n | kWalkDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             __builtin_amdgcn_s_setprio(0);
           }
+          for (;;) {
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(s_claim, 1u);
+            k = uni(k);
+            uint32_t pub;
+            for (;;) {
+              pub = uni(__hip_atomic_load(s_pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+              if (k < (pub & ~kWalkDone) || (pub & kWalkDone)) break;
+              __builtin_amdgcn_s_sleep(1);
+            }
+            if (k >= (pub & ~kWalkDone)) break;  // the walk is done and every run is claimed
+            expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][k]), vi + uni(s_val[0][k]), is_signed,
+                             value_begin, value_end, dst, lane);
+          }
+          // the other parity's counters are idle: clear them for the next serial pass
+          if (tid == 0) {
+            s_sync[sync_par ^ 1][0] = 0;
+            s_sync[sync_par ^ 1][1] = 0;
+          }
+          sync_par ^= 1;
           __syncthreads();
-          PROF_MARK(1);
           n = uni(s_ctl[0][0]);
           stop = uni(s_ctl[0][1]);
           dpos = uni(s_ctl[0][2]);
           dval = uni(s_ctl[0][3]);
-          for (uint32_t k = wave; k < n; k += kWaves)
-            expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][k]), vi + uni(s_val[0][k]), is_signed,
-                             value_begin, value_end, dst, lane);
         }
         __syncthreads();  // the run table (and the window) are rewritten next
         PROF_MARK(was_dense ? 6 : 2);
