@@ -37,13 +37,13 @@ def main():
         L.orcg_probe_copy(ctx.handle, orc_amd.rle._tensor_ptr(d_vals), orc_amd.rle._tensor_ptr(d_copy), 8 * n, 2)
 
     for name, fn in [("decode", dec), ("copy8nt", cpy), ("decode", dec), ("copy8nt", cpy)]:
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(61)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(201)]
         ev[0].record(stream)
-        for i in range(60):
+        for i in range(200):
             fn()
             ev[i + 1].record(stream)
         ev[-1].synchronize()
-        ts = [ev[i].elapsed_time(ev[i + 1]) * 1000 for i in range(60)]
+        ts = [ev[i].elapsed_time(ev[i + 1]) * 1000 for i in range(200)]
         print(json.dumps({"kernel": name, "us": [round(t, 1) for t in ts]}), flush=True)
 
 
