@@ -2,7 +2,9 @@
 //
 // One 256-thread workgroup per segment. The segment's bytes stream through an
 // LDS window filled by buffer_load ... lds (LDS-DMA, 1 KB per wave
-// instruction, range-checked so reads past the stream return zeros). The run
+// instruction, range-checked so reads past the stream return zeros), or, in
+// the wide-value instance, by 16-byte buffer loads into registers that are
+// all in flight before the LDS writes (kOptRegFill). The run
 // headers are walked in LDS (RleDecoderV2::next's run loop,
 // c++/src/RleDecoderV2.cc:132-170) into a run table, and waves expand runs
 // round-robin straight out of LDS:
@@ -79,6 +81,7 @@ constexpr int kOptNTStore = 1;  // non-temporal output stores (streamed, never r
 constexpr int kOptNTLoad = 2;   // non-temporal LDS-DMA loads of the stream
 constexpr int kOptReuse = 4;    // carry the window tail over in LDS; never load past the segment
 constexpr int kOptFast = 8;     // predicate-free path for full DIRECT runs inside the output range
+constexpr int kOptRegFill = 16; // fill windows through registers (16 B buffer loads, then LDS writes), not LDS-DMA
 
 template <int kOpt, typename T>
 __device__ __forceinline__ void store1(T* p, uint64_t v) {
@@ -801,7 +804,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   constexpr uint32_t kCap = kDense ? kDenseRuns : 512u;
   static_assert(!kDense || 2 * kCap >= kSlab, "DP table must fit the run table");
   static_assert(!kDense || kChunk >= kSlab, "window too small for a slab");
-  __shared__ uint32_t s_win[kBufs][kWin / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
+  __shared__ __attribute__((aligned(16))) uint32_t s_win[kBufs][kWin / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
   __shared__ uint32_t s_tab[kBufs][2 * kCap];
   __shared__ uint32_t s_ctl[kBufs][12];
   __shared__ uint32_t s_sync[2][2];  // serial passes: {published runs, claimed runs}, by pass parity
@@ -873,11 +876,30 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             *(u4*)((char*)s_win[0] + o) = *(const u4*)((const char*)s_win[0] + so + o);
           __syncthreads();  // reads of the tail finish before the DMA below lands
         }
-        for (uint32_t off = keep + wave * 1024u; off < need; off += kWaves * 1024u)
-          if (off + lane * 16u < need)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                rs, (__attribute__((address_space(3))) void*)((char*)s_win[0] + off), 16,
-                wrel + off + lane * 16u, 0, 0, (kOpt & kOptNTLoad) ? 2 : 0);
+        if constexpr ((kOpt & kOptRegFill) != 0) {
+          // every lane issues all of its 16-byte loads before the first LDS
+          // write (measured: +4 % over LDS-DMA on a pure window copy)
+          typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+          constexpr int kPer = (kWin + kThreads * 16 - 1) / (kThreads * 16);
+          u4 v[kPer];
+#pragma unroll
+          for (int i = 0; i < kPer; ++i) {
+            const uint32_t off = keep + (uint32_t)(i * kThreads + tid) * 16u;
+            if (off < need)
+              v[i] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, wrel + off, 0, 2));
+          }
+#pragma unroll
+          for (int i = 0; i < kPer; ++i) {
+            const uint32_t off = keep + (uint32_t)(i * kThreads + tid) * 16u;
+            if (off < need) *(u4*)((char*)s_win[0] + off) = v[i];
+          }
+        } else {
+          for (uint32_t off = keep + wave * 1024u; off < need; off += kWaves * 1024u)
+            if (off + lane * 16u < need)
+              __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                  rs, (__attribute__((address_space(3))) void*)((char*)s_win[0] + off), 16,
+                  wrel + off + lane * 16u, 0, 0, (kOpt & kOptNTLoad) ? 2 : 0);
+        }
       } else {
         fill<kOpt>(s_win[0], rs, wrel, kWin, wave, kWaves, lane);
       }
@@ -1069,10 +1091,13 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
     case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true); break;  // dense-capable, 13 KB
     case 12: ORCG_KT(kOptNTStore | kOptFast, 21, true, 3, false); break;               // producer wave, 2 x 21 KB
     case 13: ORCG_KT(kOptNTStore | kOptFast, 13, true, 4, false); break;               // producer wave, 2 x 13 KB
+    case 14: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false); break;             // 9 + register fill
     default: {
       // ORCG_RLEV2_TILED picks the instance by stream density: wide values
       // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
-      // 33 KB windows (4 WG/CU); narrower ones need more workgroups in
+      // 33 KB windows (4 WG/CU) filled through registers (+2 % over
+      // LDS-DMA; the 21 KB instance cannot hold its loads without spilling
+      // at 6 WG/CU); narrower ones need more workgroups in
       // flight per CU to keep HBM busy: 21 KB windows (6 WG/CU) + the
       // predicate-free full-run path; below 1.25 bytes per value the stream
       // may be made of short runs (low-cardinality columns: SHORT_REPEAT runs
@@ -1081,7 +1106,7 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
       // narrow long-run streams (its LDS allows 5 WG/CU, not 6). Measured:
       // scripts/ab_rlev2.py, profiles/r01/sweep.md.
       const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
-      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false);
+      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false);
       else if (4 * src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false);
       else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true);
       break;

@@ -110,7 +110,14 @@ def main():
             bad.append(var)
     keep = {int(x) for x in args.timing_only.split(",") if x}
     variants = [v for v in variants if v not in bad or v in keep]
-    refs = ["copy", "probe0", "probe1", "probe2", "probe3", "probe4", "probe5", "probe6"]
+    refs = ["copy", "probe0", "probe1", "probe2", "probe3", "probe4", "probe5", "probe6", "probe7", "probe8", "probe9", "probe10", "probe11"]
+    for var in refs[1:]:
+        with torch.cuda.stream(stream):
+            d_copy.zero_()
+        run(var)
+        ctx.synchronize()
+        if not torch.equal(d_copy, d_vals):
+            print(json.dumps({"variant": var, "mismatch": int((d_copy != d_vals).sum())}), flush=True)
     times = {var: [] for var in refs + variants}
     for _ in range(args.rounds):
         for var in refs + variants:
