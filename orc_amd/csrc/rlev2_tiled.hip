@@ -475,7 +475,7 @@ __device__ __forceinline__ uint32_t checked_run(const uint32_t* win, uint32_t lq
 // window offset of `pos`, a run start) into s_off/s_val, with the serial
 // walk's stop rules (segment end, value end, first corrupt run). All threads.
 __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint32_t* s_dp, uint32_t* s_off,
-                                                      uint32_t* s_val, uint16_t* s_nxt, uint8_t* s_mark,
+                                                      uint32_t* s_val, uint16_t* s_nxt, uint32_t* s_mark,
                                                       uint32_t* s_ctl, uint64_t wpos, uint32_t sb, uint32_t lim,
                                                       uint64_t vi, uint64_t seg_end, uint64_t src_len,
                                                       uint64_t value_end, uint32_t need, int is_signed,
@@ -565,7 +565,8 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
   // slab). Level i marks N^(2^i) of every marked position and squares N, so
   // after 8 levels the first 256 chain elements (one per block at most) are
   // marked. Marks only grow and every marked position is a chain element, so
-  // reading a mark another thread sets in the same level is harmless.
+  // reading a mark another thread sets in the same level is harmless (marks
+  // are bits of 32-bit words, set with LDS atomics).
   {
     uint16_t* na = s_nxt;
     uint16_t* nb = s_nxt + kSlab;
@@ -573,8 +574,8 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
     for (uint32_t e = 0; e < kBlk; ++e) {
       const uint32_t q = lo + e, t = s_dp[q], x = t & 0x7fffu;
       na[q] = ((t & kDpErr) || x >= lim) ? kSink : (uint16_t)x;
-      s_mark[q] = q == 0;
     }
+    if (tid < (int)(kSlab / 32)) s_mark[tid] = tid == 0;  // position 0 is the chain's start
     __syncthreads();
 #pragma unroll 1
     for (int lev = 0; lev < 8; ++lev) {
@@ -582,7 +583,7 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
       for (uint32_t e = 0; e < kBlk; ++e) {
         const uint32_t q = lo + e, n = na[q];
         if (n != kSink) {
-          if (s_mark[q]) s_mark[n] = 1;
+          if ((s_mark[q >> 5] >> (q & 31u)) & 1u) atomicOr(&s_mark[n >> 5], 1u << (n & 31u));
           nb[q] = na[n];
         } else {
           nb[q] = kSink;
@@ -598,10 +599,9 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
   // (3) block b's entry = its marked position; values before it = exclusive
   // scan of the entries' value counts. Every thread walks its block from its
   // entry with the exact checks: count, then emit.
-  uint32_t eb = kNone;
-#pragma unroll
-  for (uint32_t e = kBlk; e-- > 0;)
-    if (s_mark[lo + e]) eb = lo + e;
+  static_assert(kBlk == 8, "a block's marks are one byte of a mark word");
+  const uint32_t mb = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
+  const uint32_t eb = mb ? lo + (uint32_t)__builtin_ctz(mb) : kNone;
   const uint32_t cb = (eb != kNone && !(s_dp[eb] & kDpErr)) ? s_dp[eb] >> 15 : 0u;
   uint32_t* s_wsum = s_ctl + 4;
   const uint32_t cincl = wave_scan_u32(cb);
@@ -775,7 +775,7 @@ struct DenseLds {
     uint64_t stage[kThreads / kWave][kStage];  // expansion: per-wave value stages
     uint16_t nxt[2][kSlab];                    // discovery: chain successors (double-buffered)
   };
-  uint8_t mark[kSlab];                         // discovery: chain marks
+  uint32_t mark[kSlab / 32];                   // discovery: chain marks, one bit per position
 };
 template <>
 struct DenseLds<false> {};
@@ -786,7 +786,7 @@ __device__ __forceinline__ uint16_t* s_dense_nxt(DenseLds<kDense>& d) {
   else return nullptr;
 }
 template <bool kDense>
-__device__ __forceinline__ uint8_t* s_dense_mark(DenseLds<kDense>& d) {
+__device__ __forceinline__ uint32_t* s_dense_mark(DenseLds<kDense>& d) {
   if constexpr (kDense) return d.mark;
   else return nullptr;
 }
@@ -796,8 +796,11 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint8_t* __restrict__ src, uint64_t src_len, int is_signed,
     const uint64_t* __restrict__ segtab, uint64_t nsegs, uint64_t rows_per_group,
     uint64_t value_begin, uint64_t nvalues, T* __restrict__ dst, unsigned long long* err) {
-  constexpr uint32_t kWin = kWinKB * 1024u;
+  // dense instances get 512 B more so the window's run-start chunk is a
+  // whole number of 2 KB slabs (no partially occupied discovery pass)
+  constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
   constexpr uint32_t kChunk = kWin - kMaxRun;
+  static_assert(!kDense || kChunk % kSlab == 0, "dense window chunk must be whole slabs");
   constexpr int kBufs = kPipe ? 2 : 1;
   static_assert(!(kDense && kPipe), "dense mode is a non-pipelined instance");
   // run table capacity; in dense instances the slab DP table aliases it
@@ -1087,11 +1090,12 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
   switch (ctx->rlev2_variant) {
     case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false); break;  // 21 KB + fast
     case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
-    case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 4, true); break;  // dense-capable, 21 KB
-    case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true); break;  // dense-capable, 13 KB
+    case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 20, false, 4, true); break;  // dense-capable, 20.5 KB
+    case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 12, false, 5, true); break;  // dense-capable, 12.5 KB
     case 12: ORCG_KT(kOptNTStore | kOptFast, 21, true, 3, false); break;               // producer wave, 2 x 21 KB
     case 13: ORCG_KT(kOptNTStore | kOptFast, 13, true, 4, false); break;               // producer wave, 2 x 13 KB
     case 14: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false); break;             // 9 + register fill
+    case 15: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 8, false, 6, true); break;    // dense-capable, 8.5 KB, 6 WG/CU
     default: {
       // ORCG_RLEV2_TILED picks the instance by stream density: wide values
       // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
@@ -1101,14 +1105,18 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
       // flight per CU to keep HBM busy: 21 KB windows (6 WG/CU) + the
       // predicate-free full-run path; below 1.25 bytes per value the stream
       // may be made of short runs (low-cardinality columns: SHORT_REPEAT runs
-      // are 0.2-1 B/value), so the instance with the dense (parallel run
-      // discovery) mode runs: 5x faster on such streams, <= 15 % slower on
-      // narrow long-run streams (its LDS allows 5 WG/CU, not 6). Measured:
-      // scripts/ab_rlev2.py, profiles/r01/sweep.md.
+      // are 0.2-1 B/value), so an instance with the dense (parallel run
+      // discovery) mode runs: 5x faster on such streams. Its LDS (window +
+      // run table / DP table + stages / chain tables) sets the occupancy:
+      // 12.5 KB windows (5 WG/CU) from 0.75 B/value, 8.5 KB windows (6 WG/CU,
+      // +10 % on SHORT_REPEAT streams, -4..7 % on W=8 DIRECT / narrow DELTA
+      // from the extra window moves) below. Measured: scripts/ab_rlev2.py,
+      // profiles/r01/sweep.md.
       const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
       if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false);
       else if (4 * src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false);
-      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 13, false, 5, true);
+      else if (4 * src_len >= 3 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 12, false, 5, true);
+      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 8, false, 6, true);
       break;
     }
   }
