@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--stride", type=int, default=10_000)
     ap.add_argument("--data", default="random", choices=["random", "delta", "repeat", "patched"])
+    ap.add_argument("--refs", default="copy,probe2,probe5,probe7,probe11",
+                    help="reference copies timed beside the decoder (copy = torch, probeN = orcg_probe_copy mode N)")
     ap.add_argument("--timing-only", default="", help="variants timed even when their output mismatches (debug instances)")
     args = ap.parse_args()
     import torch
@@ -110,8 +112,8 @@ def main():
             bad.append(var)
     keep = {int(x) for x in args.timing_only.split(",") if x}
     variants = [v for v in variants if v not in bad or v in keep]
-    refs = ["copy", "probe0", "probe1", "probe2", "probe3", "probe4", "probe5", "probe6", "probe7", "probe8", "probe9", "probe10", "probe11"]
-    for var in refs[1:]:
+    refs = [r for r in args.refs.split(",") if r]
+    for var in [r for r in refs if r.startswith("probe")]:
         with torch.cuda.stream(stream):
             d_copy.zero_()
         run(var)

@@ -32,6 +32,8 @@ def counter(path, name):
 
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    if not (rnd.startswith("r") and rnd[1:].isdigit()):
+        sys.exit("usage: summarize_profiles.py rNN   (folds gpurun_out/{prof,pmc_fetch,pmc_write} into profiles/rNN)")
     src = os.path.join(ROOT, "gpurun_out")
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
