@@ -80,7 +80,7 @@ constexpr uint32_t kToDense = 24, kToSerial = 64;
 constexpr int kOptNTStore = 1;  // non-temporal output stores (streamed, never re-read)
 constexpr int kOptNTLoad = 2;   // non-temporal LDS-DMA loads of the stream
 constexpr int kOptReuse = 4;    // carry the window tail over in LDS; never load past the segment
-constexpr int kOptFast = 8;     // predicate-free path for full DIRECT runs inside the output range
+constexpr int kOptFast = 8;     // predicate-free paths for full (512-value) runs inside the output range
 constexpr int kOptRegFill = 16; // fill windows through registers (16 B buffer loads, then LDS writes), not LDS-DMA
 
 template <int kOpt, typename T>
@@ -225,6 +225,30 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
         prev = c;
         first = false;
       }
+    }
+    if ((kOpt & kOptFast) && L == 512 && v0 >= value_begin && v0 + 512 <= value_end) {
+      // full run inside the output range: all 8 chunks' literals in
+      // registers, the (few) patches OR-ed into the lane that owns their
+      // position, then predicate-free stores
+      T* out = dst + (v0 - value_begin);
+      uint64_t lit[kMaxRunUnroll];
+#pragma unroll
+      for (int it = 0; it < kMaxRunUnroll; ++it) {
+        const uint32_t bit = (uint32_t)(it * kWave + lane) * W;
+        const uint32_t br = d + (bit >> 3);
+        lit[it] = field(lds12(win, br), br, bit & 7u, W);
+      }
+      for (uint64_t t = applied; t; t &= t - 1) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(t);
+        const uint32_t c = rdlane(cum, k);
+        const uint64_t add = (((uint64_t)rdlane(p_hi, k) << 32) | rdlane(p_lo, k)) << (W & 63u);
+#pragma unroll
+        for (int it = 0; it < kMaxRunUnroll; ++it)
+          if (c == (uint32_t)(it * kWave + lane)) lit[it] |= add;
+      }
+#pragma unroll
+      for (int it = 0; it < kMaxRunUnroll; ++it) store1<kOpt>(out + it * kWave + lane, r.a + lit[it]);
+      return;
     }
     uint64_t todo = applied;
 #pragma unroll 1

@@ -256,3 +256,48 @@ def test_structured_streams_every_variant(kind):
             assert np.array_equal(got, want), "variant %d stride %d: first mismatch at %d" % (
                 variant, stride, int(np.argmax(got != want)))
     ctx.set_rlev2_variant(0)
+
+
+@pytest.mark.parametrize("layout", ["edges", "same_chunk", "escape_gaps", "max_patches"])
+def test_patched_full_runs_patch_layouts(layout):
+    """Full 512-value PATCHED_BASE runs (the predicate-free path) with patches
+    at chunk edges (0, 63, 64, 511), several in one 64-value chunk, gaps past
+    255 (escape entries, RleDecoderV2.cc:250-271) and the 31-entry maximum,
+    against the oracle, with row groups aligned to the runs and not."""
+    import torch
+
+    import orc_amd
+
+    pos_sets = {
+        "edges": [0, 1, 63, 64, 65, 127, 128, 300, 510, 511],
+        "same_chunk": [200, 201, 203, 210, 230, 255],
+        "escape_gaps": [5, 400, 511],
+        "max_patches": list(range(0, 512, 17))[:31],
+    }[layout]
+    rng = np.random.default_rng(7)
+    runs = 40
+    v = rng.integers(0, 1 << 10, size=runs * 512, dtype=np.int64)
+    for r in range(runs):
+        for p in pos_sets:
+            v[r * 512 + p] += int(rng.integers(1 << 20, 1 << 40)) << 10
+        v[r * 512 + 7] = 0  # a small base
+    data, offs = orc_amd.encode_runs(v, True, np.full(runs, 2, dtype=np.uint8), np.full(runs, 512, dtype=np.uint32))
+    want = oracle.rlev2_decode(data.tobytes(), v.size, True)
+    np.testing.assert_array_equal(want, v)
+    ctx = orc_amd.default_context(0)
+    d_src = torch.from_numpy(data).cuda()
+    starts = np.arange(runs, dtype=np.int64) * 512
+    for stride in (1024, 1000):
+        g = np.arange(0, v.size, stride)
+        ri = np.searchsorted(starts, g, side="right") - 1
+        pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
+        d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+        for variant in (0, 8, 9, 10, 11, 15):
+            ctx.set_rlev2_variant(variant)
+            out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, True, out)
+            ctx.synchronize()
+            got = out.cpu().numpy()
+            assert np.array_equal(got, want), "variant %d stride %d: first mismatch at %d" % (
+                variant, stride, int(np.argmax(got != want)))
+    ctx.set_rlev2_variant(0)
