@@ -622,7 +622,8 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
   PROF_MARK(4);
   // (3) block b's entry = its marked position; values before it = exclusive
   // scan of the entries' value counts. Every thread walks its block from its
-  // entry with the exact checks: count, then emit.
+  // entry with the exact checks, keeping its (at most 4: every run is >= 2
+  // bytes) run starts in registers, then emits them after the count scan.
   static_assert(kBlk == 8, "a block's marks are one byte of a mark word");
   const uint32_t mb = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
   const uint32_t eb = mb ? lo + (uint32_t)__builtin_ctz(mb) : kNone;
@@ -640,6 +641,8 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
   for (int w = 0; w < wave; ++w) vb += s_wsum[w];
   __syncthreads();  // s_wsum is reused by the run-count scan
   uint32_t cnt = 0, p = eb, v = vb;
+  uint32_t pk_off = 0;  // run k starts at lo + 3-bit field k
+  uint64_t pk_val = 0;  // ... with its first value at vb + 16-bit field k (<= 3 * 512)
   if (eb != kNone) {
     while (p < hi && p < lim && wpos + sb + p < seg_end && vi + v < value_end) {
       Run r;
@@ -649,6 +652,8 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
         s_ctl[3] = 1;
         break;
       }
+      pk_off |= (p - lo) << (3 * cnt);
+      pk_val |= (uint64_t)(v - vb) << (16 * cnt);
       ++cnt;
       p += r.bytes;
       v += r.L;
@@ -675,17 +680,9 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
   // the DP table is dead: the run table may overwrite it (s_dp aliases
   // s_off/s_val), but only once every thread has walked
   __syncthreads();
-  if (cnt) {
-    p = eb;
-    v = vb;
-    for (uint32_t k = 0; k < cnt; ++k) {
-      Run r;
-      checked_run(win, sb + p, wpos, seg_end, src_len, need, is_signed, &r);
-      s_off[base + k] = sb + p;
-      s_val[base + k] = v;
-      p += r.bytes;
-      v += r.L;
-    }
+  for (uint32_t k = 0; k < cnt; ++k) {
+    s_off[base + k] = sb + lo + ((pk_off >> (3 * k)) & 7u);
+    s_val[base + k] = vb + (uint32_t)((pk_val >> (16 * k)) & 0xffffu);
   }
   __syncthreads();
   PROF_MARK(5);
