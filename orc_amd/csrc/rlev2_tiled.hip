@@ -82,6 +82,7 @@ constexpr int kOptNTLoad = 2;   // non-temporal LDS-DMA loads of the stream
 constexpr int kOptReuse = 4;    // carry the window tail over in LDS; never load past the segment
 constexpr int kOptFast = 8;     // predicate-free paths for full (512-value) runs inside the output range
 constexpr int kOptRegFill = 16; // fill windows through registers (16 B buffer loads, then LDS writes), not LDS-DMA
+constexpr int kOptT4 = 32;      // walk reads DELTA varint ends from per-dword terminator nibbles computed at slice load
 
 template <int kOpt, typename T>
 __device__ __forceinline__ void store1(T* p, uint64_t v) {
@@ -108,13 +109,21 @@ __device__ __forceinline__ u32x3 lds12(const uint32_t* w, uint32_t o) {
 // (DELTA's two varints take <= 22 bytes; longer ones are corrupt).
 constexpr uint32_t kHdrLim = 64;
 
+// terminator bits of a dword's bytes (bit i = byte i < 0x80)
+__device__ __forceinline__ uint32_t term4(uint32_t w) {
+  const uint32_t m = (~w >> 7) & 0x01010101u;
+  return (m * 0x10204080u) >> 28;
+}
+
 struct LaneWin {
   uint32_t word = 0, base = 0xffffffffu;
+  uint32_t t4 = 0;  // term4(word): the walk's varint ends, computed once per slice on the VALU
   __device__ __forceinline__ void load(const uint32_t* win, uint32_t hoff, uint32_t nwords, int lane) {
     base = hoff & ~3u;
     uint32_t idx = (base >> 2) + (uint32_t)lane;
     if (idx >= nwords) idx = nwords - 1;
     word = win[idx];
+    t4 = term4(word);
   }
   // make sure [hoff, hoff + kHdrLim) is inside the slice
   __device__ __forceinline__ void cover(const uint32_t* win, uint32_t hoff, uint32_t nwords, int lane) {
@@ -133,7 +142,51 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
                                            int lane) {
   LaneWin hw;
   hw.load(win, hoff, nwords, lane);
-  const Run r = parse_run([&](uint32_t i) { return hw.byte(hoff + i); }, ~0ull, kHdrLim, is_signed);
+  Run r;
+  if ((hw.byte(hoff) >> 6) == 3) {
+    // DELTA header of a run the walk validated, one header byte per lane: varint
+    // ends from a ballot of the terminator bytes, values OR-reduced in the
+    // DPP rows, instead of a
+    // scalar byte loop (the kernel's scalar unit is its busiest on DELTA
+    // streams)
+    const uint32_t fb = hw.byte(hoff);
+    r.kind = 3;
+    r.pbs = r.pl = r.cfb = 0;
+    r.err = kErrNone;
+    r.L = ((fb & 1u) << 8 | hw.byte(hoff + 1)) + 1u;
+    const uint32_t fbo = (fb >> 1) & 0x1fu;
+    r.W = fbo ? fbs_width(fbo) : 0u;
+    const uint32_t hb = lds_byte(win, hoff + 2u + (uint32_t)lane);
+    const uint64_t term = __ballot(hb < 0x80u);
+    const uint32_t n1 = (uint32_t)__builtin_ctzll(term) + 1u;
+    const uint32_t n2 = (uint32_t)__builtin_ctzll(term >> n1) + 1u;
+    const uint32_t b7 = hb & 0x7fu, k2 = (uint32_t)lane - n1;
+    uint64_t ca = ((uint32_t)lane < n1 && lane < 10) ? (uint64_t)b7 << (7 * lane) : 0ull;
+    uint64_t cb = ((uint32_t)lane >= n1 && k2 < n2 && k2 < 10u) ? (uint64_t)b7 << (7 * k2) : 0ull;
+#define ORCG_OR_ROWS(x)                  \
+  x |= dpp0_64<0x111, 0xf>(x);           \
+  x |= dpp0_64<0x112, 0xf>(x);           \
+  x |= dpp0_64<0x114, 0xf>(x);           \
+  x |= dpp0_64<0x118, 0xf>(x)
+    ORCG_OR_ROWS(ca);
+    ORCG_OR_ROWS(cb);
+#undef ORCG_OR_ROWS
+    // the row totals sit in lanes 15 / 31 / 47 / 63 (a header reaches 64 bytes)
+    auto rows_or = [](uint64_t x) -> uint64_t {
+      const uint32_t lo = rdlane((uint32_t)x, 15) | rdlane((uint32_t)x, 31) | rdlane((uint32_t)x, 47) |
+                          rdlane((uint32_t)x, 63);
+      const uint32_t hi = rdlane((uint32_t)(x >> 32), 15) | rdlane((uint32_t)(x >> 32), 31) |
+                          rdlane((uint32_t)(x >> 32), 47) | rdlane((uint32_t)(x >> 32), 63);
+      return ((uint64_t)hi << 32) | lo;
+    };
+    const uint64_t a_raw = rows_or(ca), b_raw = rows_or(cb);
+    r.a = is_signed ? unzigzag(a_raw) : a_raw;
+    r.b = unzigzag(b_raw);
+    r.data = 2u + n1 + n2;
+    r.bytes = r.data + (r.W ? (r.W * (r.L - 2u) + 7u) / 8u : 0u);
+  } else {
+    r = parse_run([&](uint32_t i) { return hw.byte(hoff + i); }, ~0ull, kHdrLim, is_signed);
+  }
   const uint32_t L = r.L;
   if (v0 + L <= value_begin || v0 >= value_end) return;  // outside the requested rows
   const uint32_t d = hoff + r.data;  // LDS offset of the packed data
@@ -365,17 +418,12 @@ struct WalkResult {
   uint32_t n, stop, dpos, dval;
 };
 
-// terminator bits of a dword's bytes (bit i = byte i < 0x80)
-__device__ __forceinline__ uint32_t term4(uint32_t w) {
-  const uint32_t m = (~w >> 7) & 0x01010101u;
-  return (m * 0x10204080u) >> 28;
-}
-
 // The serial walk's view of a run: bytes, values and the error parse_run
 // would report, in its order. SHORT_REPEAT / DIRECT from the first two
 // bytes, DELTA from a terminator mask of the 24 bytes after its header
 // (two varints of <= 11 bytes: every writer's); PATCHED_BASE and longer
 // varints through parse_run.
+template <bool kT4>
 __device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint64_t avail, int is_signed,
                                             uint32_t* bytes, uint32_t* L, uint32_t* err) {
   const uint32_t fb = hw.byte(lp), kind = fb >> 6;
@@ -402,13 +450,21 @@ __device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint
       return;
     }
     // DELTA: varint lengths from the terminator mask of bytes lp+2 .. lp+25
+    // (the slice's per-dword terminator nibbles, gathered and realigned)
     const uint32_t o = lp + 2u - hw.base, i0 = o >> 2, sh = o & 3u;
-    uint32_t t = 0, prev = rdlane(hw.word, i0);
+    uint32_t t = 0;
+    if constexpr (kT4) {
 #pragma unroll
-    for (uint32_t k = 0; k < 6; ++k) {
-      const uint32_t nx = rdlane(hw.word, i0 + k + 1);
-      t |= term4(__builtin_amdgcn_alignbyte(nx, prev, sh)) << (4 * k);
-      prev = nx;
+      for (uint32_t k = 0; k < 7; ++k) t |= rdlane(hw.t4, i0 + k) << (4 * k);
+      t = (t >> sh) & 0xffffffu;
+    } else {
+      uint32_t prev = rdlane(hw.word, i0);
+#pragma unroll
+      for (uint32_t k = 0; k < 6; ++k) {
+        const uint32_t nx = rdlane(hw.word, i0 + k + 1);
+        t |= term4(__builtin_amdgcn_alignbyte(nx, prev, sh)) << (4 * k);
+        prev = nx;
+      }
     }
     const uint32_t n1 = t ? (uint32_t)__builtin_ctz(t) + 1u : 32u;
     const uint32_t t2 = n1 < 24 ? t >> n1 : 0u;
@@ -438,7 +494,7 @@ __device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint
 // Wave-uniform header walk over the window [wpos, wpos + kWin): records runs
 // starting at pos.. into (run_off, run_val) until the next run starts past
 // kWin - kMaxRun, leaves the segment, or the table is full.
-template <uint32_t kWin, uint32_t kCap>
+template <uint32_t kWin, uint32_t kCap, bool kT4 = false>
 __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_off, uint32_t* run_val,
                                            uint64_t wpos, uint64_t pos, uint64_t vi, uint64_t seg_end,
                                            uint64_t src_len, uint64_t value_end, int is_signed,
@@ -453,7 +509,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
     if (lp >= kChunk && n > 0) break;  // starts in the next window
     hw.cover(win, lp, kWin / 4 + 8, lane);
     uint32_t rbytes, rL, e;
-    walk_extent(hw, lp, src_len - p, is_signed, &rbytes, &rL, &e);
+    walk_extent<kT4>(hw, lp, src_len - p, is_signed, &rbytes, &rL, &e);
     if (e == kErrNone && p + rbytes > seg_end) e = kErrBadSegment;
     if (e == kErrNone && lp + rbytes > lim) e = kErrBadRead;  // only a corrupt varint gets here
     if (e != kErrNone) {
@@ -968,8 +1024,9 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             // dense instances: a short first walk (the probe) measures the
             // stream's bytes per run before committing to a mode
             const uint32_t cap = (kDense && probe) ? 32u : kCap;
-            const WalkResult w = walk<kWin, kCap>(s_win[0], s_off[0], s_val[0], wpos, pos, vi, seg_end, src_len,
-                                                  value_end, is_signed, err, lane, need, cap, s_pub);
+            const WalkResult w = walk<kWin, kCap, (kOpt & kOptT4) != 0>(s_win[0], s_off[0], s_val[0], wpos, pos, vi,
+                                                                    seg_end, src_len, value_end, is_signed, err,
+                                                                    lane, need, cap, s_pub);
             if (lane == 0) {
               s_ctl[0][0] = w.n;
               s_ctl[0][1] = w.stop;
@@ -1117,6 +1174,10 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
     case 13: ORCG_KT(kOptNTStore | kOptFast, 13, true, 4, false); break;               // producer wave, 2 x 13 KB
     case 14: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false); break;             // 9 + register fill
     case 15: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 8, false, 6, true); break;    // dense-capable, 8.5 KB, 6 WG/CU
+    case 16: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 21, false, 6, false); break;  // 8 + T4
+    case 17: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptT4, 33, false, 1, false); break; // 14 + T4
+    case 18: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 12, false, 5, true); break;    // 11 + T4
+    case 19: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 8, false, 6, true); break;     // 15 + T4
     default: {
       // ORCG_RLEV2_TILED picks the instance by stream density: wide values
       // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
@@ -1131,13 +1192,15 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
       // run table / DP table + stages / chain tables) sets the occupancy:
       // 12.5 KB windows (5 WG/CU) from 0.75 B/value, 8.5 KB windows (6 WG/CU,
       // +10 % on SHORT_REPEAT streams, -4..7 % on W=8 DIRECT / narrow DELTA
-      // from the extra window moves) below. Measured: scripts/ab_rlev2.py,
+      // from the extra window moves) below. All but the 33 KB instance walk
+      // DELTA headers through per-dword terminator nibbles (kOptT4: +5-7 % on
+      // DELTA streams, neutral elsewhere). Measured: scripts/ab_rlev2.py,
       // profiles/r01/sweep.md.
       const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
       if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false);
-      else if (4 * src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false);
-      else if (4 * src_len >= 3 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 12, false, 5, true);
-      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 8, false, 6, true);
+      else if (4 * src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 21, false, 6, false);
+      else if (4 * src_len >= 3 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 12, false, 5, true);
+      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 8, false, 6, true);
       break;
     }
   }

@@ -27,9 +27,9 @@ for s in $STEPS; do
     ab) run ab 600 python scripts/ab_rlev2.py --variants 0,1,8,9 ;;
     ab13) run ab13 600 python scripts/ab_rlev2.py --bits 13 --variants 0,1,8,9 ;;
     sweep)
-      for b in 1 8 13 24 32 48 64; do run sweep_w$b 300 python scripts/ab_rlev2.py --bits $b --variants 0,1,8,9,10,11,14,15 --rounds 3 || true; done
-      for d in delta repeat patched; do run sweep_$d 300 python scripts/ab_rlev2.py --data $d --bits 12 --variants 0,1,8,9,10,11,14,15 --rounds 3 || true; done
-      run sweep_repeat40 300 python scripts/ab_rlev2.py --data repeat --bits 40 --variants 0,1,8,9,10,11,14,15 --rounds 3 || true ;;
+      for b in 1 8 13 24 32 48 64; do run sweep_w$b 300 python scripts/ab_rlev2.py --bits $b --variants 0,1,8,9,10,11,14,15,16,18,19 --rounds 3 || true; done
+      for d in delta repeat patched; do run sweep_$d 300 python scripts/ab_rlev2.py --data $d --bits 12 --variants 0,1,8,9,10,11,14,15,16,18,19 --rounds 3 || true; done
+      run sweep_repeat40 300 python scripts/ab_rlev2.py --data repeat --bits 40 --variants 0,1,8,9,10,11,14,15,16,18,19 --rounds 3 || true ;;
     benchwalk) run bench_walk 600 python bench.py --variant 1 --no-cpu-baseline ;;
     prof)
       export TMPDIR=/tmp

@@ -21,6 +21,10 @@ VARIANTS = {
     11: "dense-capable 12.5 KB",
     14: "tiled 33 KB, register fill",
     15: "dense-capable 8.5 KB (6 WG/CU)",
+    16: "8 + DELTA varint ends from terminator nibbles (T4)",
+    17: "14 + T4",
+    18: "11 + T4",
+    19: "15 + T4",
 }
 REFS = {
     "copy": "torch copy",

@@ -12,7 +12,7 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-DENSE_VARIANTS = [0, 10, 11, 15]  # default (dense below 1.25 B/value), dense 21 KB, dense 13 KB, dense 10 KB (6 WG/CU)
+DENSE_VARIANTS = [0, 10, 11, 15, 18, 19]  # default (dense below 1.25 B/value), dense 21 KB, dense 13 KB, dense 10 KB (6 WG/CU), 11 / 15 + T4
 
 
 def _short_run_stream(rng, signed, n_target, long_every=0):
