@@ -219,7 +219,7 @@ int orcg_ctx_set_stream(orcg_ctx* c, void* s) {
 int orcg_ctx_set_rlev2_variant(orcg_ctx* c, int v) {
   // 0 tiled (default), 1 wave-walk; 8..19 pin one tiled instance
   // (rlev2_tiled.hip launch_rlev2_tiled), the others run the default
-  if (!c || v < 0 || v > 19) return ORCG_INVALID_ARGUMENT;
+  if (!c || v < 0 || v > 20) return ORCG_INVALID_ARGUMENT;
   c->rlev2_variant = v;
   return ORCG_OK;
 }

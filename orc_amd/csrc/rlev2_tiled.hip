@@ -1178,6 +1178,7 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
     case 17: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptT4, 33, false, 1, false); break; // 14 + T4
     case 18: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 12, false, 5, true); break;    // 11 + T4
     case 19: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 8, false, 6, true); break;     // 15 + T4
+    case 20: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptFast | kOptT4, 33, false, 1, false); break; // 17 + full-run fast paths
     default: {
       // ORCG_RLEV2_TILED picks the instance by stream density: wide values
       // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
@@ -1192,12 +1193,14 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
       // run table / DP table + stages / chain tables) sets the occupancy:
       // 12.5 KB windows (5 WG/CU) from 0.75 B/value, 8.5 KB windows (6 WG/CU,
       // +10 % on SHORT_REPEAT streams, -4..7 % on W=8 DIRECT / narrow DELTA
-      // from the extra window moves) below. All but the 33 KB instance walk
+      // from the extra window moves) below. Every instance walks
       // DELTA headers through per-dword terminator nibbles (kOptT4: +5-7 % on
       // DELTA streams, neutral elsewhere). Measured: scripts/ab_rlev2.py,
-      // profiles/r01/sweep.md.
+      // profiles/r01/sweep.md; the 33 KB instance also carries the full-run
+      // fast paths (variant 20: +1 % W=64, +5 % W=32, +42 % DELTA, +18 % PATCHED
+      // over variant 17).
       const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
-      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false);
+      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptFast | kOptT4, 33, false, 1, false);
       else if (4 * src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 21, false, 6, false);
       else if (4 * src_len >= 3 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 12, false, 5, true);
       else ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 8, false, 6, true);

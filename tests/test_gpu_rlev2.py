@@ -292,7 +292,7 @@ def test_patched_full_runs_patch_layouts(layout):
         ri = np.searchsorted(starts, g, side="right") - 1
         pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
         d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
-        for variant in (0, 8, 9, 10, 11, 15, 16, 17, 18, 19):
+        for variant in (0, 8, 9, 10, 11, 15, 16, 17, 18, 19, 20):
             ctx.set_rlev2_variant(variant)
             out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
             orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, True, out)
