@@ -7,20 +7,32 @@ DIRECT runs of 512 at W=64 (the reference writer's aligned widths), the
 uncompressed DATA stream and its ROW_INDEX positions (stride 10,000) resident
 in HBM. One step = one decode of the whole stream into an int64 column in HBM.
 
-Multi-GPU (torch.distributed.run, one rank per GPU): stripes shard across
-ranks, each rank decodes its own 10^8-row stripe, no collective in the timed
-region ("scaling": "weak"); value = all rows decoded / max-over-ranks time.
+Multi-GPU: `--gpus N` (N > 1) run without torch.distributed.run's environment
+starts N ranks itself (a child `python -m torch.distributed.run`, spawned
+before this process touches the GPU); under torch.distributed.run each rank
+owns one GPU. Stripes shard across ranks as RowReaderOptions::range does
+(c++/src/Reader.cc:337-345): each rank decodes its own 10^8-row stripe, no
+collective in the timed region ("scaling": "weak"); value = all rows decoded
+/ max-over-ranks time. Outside the timed region the final row-batch concat
+is measured both ways SURVEY.md §8(e) names: every rank D2H's its rows into
+its own slice of one shared host batch (no collective), and an RCCL
+point-to-point gather of the device columns to rank 0 over xGMI.
 
 The JSON line also carries
   roofline     achieved algorithmic bytes (S + 8N per launch) / the kernel's
                HIP-event duration on its own stream, vs 8 TB/s HBM3E peak;
   cpu_baseline the CPU oracle (oracle/orc_oracle.c, a scalar restatement of
-               RleDecoderV2) timed on this host on a bounded sample.
+               RleDecoderV2) timed on this host on a bounded sample, on all
+               usable cores (independent streams) beside 1 core; the
+               reference's own AVX-512 figures from BASELINE.md as context.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -30,6 +42,12 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "decoded GB/s + Mvalues/s device-resident, RLEv2 int64 column at 1/2/4/8 GPU"
+# The reference's RleDecoderV2 on the survey container's Xeon (BASELINE.md §2,
+# W=64, N=10^8): quoted for context, not measured here (the reference source
+# does not travel to the GPU host)
+REFERENCE_CPU = {"source": "BASELINE.md §2 (reference RleDecoderV2, survey container: 8 vCPU Xeon, not this host)",
+                 "w64_1core_none_mvalues_per_s": 413.7, "w64_1core_avx512_mvalues_per_s": 473.2,
+                 "w64_8core_avx512_mvalues_per_s": 3895.0}
 
 
 def make_stream(rows, stride, seed=42):
@@ -41,34 +59,68 @@ def make_stream(rows, stride, seed=42):
     return v, data, pos
 
 
+def usable_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    # the GPU box's share is 16 CPUs whatever nproc shows
+    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
+
+
 def cpu_baseline(data, rows, budget_s):
-    """Scalar C oracle, 1 thread, on a bounded sample of the same stream:
-    the first `sample` rows, repeated until ~budget_s of CPU work."""
+    """Scalar C oracle on a bounded sample of the same stream: the first
+    `sample` rows (a run-aligned stream prefix), decoded repeatedly, on one
+    core and then on every usable core at once (one independent stream per
+    thread; ctypes releases the GIL around the C call)."""
     from oracle import oracle
 
-    sample = min(rows, 20_000_000)
-    # the sample's stream prefix ends at the first run boundary after `sample`
-    buf = data.tobytes()
-    out = np.empty(sample, dtype=np.int64)
     lib = oracle.lib()
-    src = np.frombuffer(buf, dtype=np.uint8)
-    reps, t_total = 0, 0.0
-    while t_total < budget_s or reps == 0:
+    src = np.frombuffer(data.tobytes(), dtype=np.uint8)
+
+    def leg(threads, sample, seconds):
+        outs = [np.empty(sample, dtype=np.int64) for _ in range(threads)]
+        done = [0] * threads
+        err = []
+        stop = time.perf_counter() + seconds
+
+        def work(t):
+            while True:
+                rc = lib.orco_rlev2_decode_i64(src.ctypes.data, src.size, 1, outs[t].ctypes.data, sample)
+                if rc != 0:
+                    err.append(rc)
+                    return
+                done[t] += 1
+                if time.perf_counter() >= stop:
+                    return
+
         t0 = time.perf_counter()
-        rc = lib.orco_rlev2_decode_i64(src.ctypes.data, src.size, 1, out.ctypes.data, sample)
-        t_total += time.perf_counter() - t0
-        reps += 1
-        if rc != 0:
+        ths = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        el = time.perf_counter() - t0
+        if err:
             raise RuntimeError("oracle decode failed")
-    vps = sample * reps / t_total
+        return sample * sum(done) / el, sum(done), el
+
+    cores = usable_cores()
+    s1 = min(rows, 20_000_000)
+    v1, reps1, el1 = leg(1, s1, budget_s / 2)
+    sn = min(rows, 5_000_000)
+    vn, repsn, eln = leg(cores, sn, budget_s / 2)
     return {
-        "value": round(vps * 8 / 1e9, 3),
+        "value": round(vn * 8 / 1e9, 3),
         "unit": "GB/s",
-        "mvalues_per_s": round(vps / 1e6, 1),
-        "cores": 1,
+        "mvalues_per_s": round(vn / 1e6, 1),
+        "cores": cores,
         "kind": "port",
-        "sample": "first %d rows of the same W=64 DIRECT stream, decoded %d times (%.1f s)"
-                  % (sample, reps, t_total),
+        "sample": "%d threads x first %d rows of the same W=64 DIRECT stream (independent streams), %d decodes "
+                  "in %.1f s" % (cores, sn, repsn, eln),
+        "one_core": {"value": round(v1 * 8 / 1e9, 3), "mvalues_per_s": round(v1 / 1e6, 1), "cores": 1,
+                     "sample": "first %d rows decoded %d times (%.1f s)" % (s1, reps1, el1)},
+        "reference_context": REFERENCE_CPU,
     }
 
 
@@ -84,6 +136,88 @@ def load_traffic():
     return None
 
 
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc):
+    """Start `nproc` ranks of this script under torch.distributed.run as a
+    child process (this process has not touched the GPU) and return its exit
+    code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % nproc,
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def concat_legs(dist, d_out, N, world, rank, stream):
+    """The final row-batch concat, timed outside the decode region:
+    host  -- each rank copies its rows into its own slice of one shared host
+             batch (a /dev/shm file every rank maps; offsets from an
+             all-gather of the row counts): no collective on the data;
+    rccl  -- point-to-point gather of the device columns to rank 0
+             (orc_amd.shard.gather_to_root: RCCL send/recv over xGMI)."""
+    import torch
+
+    from orc_amd.shard import gather_to_root, write_rows_to_shared_host
+
+    res = {}
+    # the shared batch lives in /dev/shm when it fits there, else in TMPDIR
+    need = 8 * N * world + (64 << 20)
+    base = "/dev/shm"
+    try:
+        st = os.statvfs(base)
+        if st.f_bavail * st.f_frsize < need:
+            base = os.environ.get("TMPDIR", "/tmp")
+    except OSError:
+        base = os.environ.get("TMPDIR", "/tmp")
+    path = os.path.join(base, "orcg_bench_concat_%s" % os.environ.get("MASTER_PORT", "0"))
+    try:
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        write_rows_to_shared_host(dist, d_out, path, create=(rank == 0))
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        res["host"] = {"ms": round(el * 1e3, 3), "GBps": round(8 * N * world / el / 1e9, 2),
+                       "bytes": 8 * N * world}
+    except Exception as e:  # reported, never fatal to the decode measurement
+        res["host"] = {"error": str(e)[:200]}
+    finally:
+        dist.barrier()
+        if rank == 0 and os.path.exists(path):
+            os.unlink(path)
+    try:
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            full = gather_to_root(dist, d_out)
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = time.perf_counter() - t0
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+        ok = True
+        if rank == 0:
+            ok = full is not None and full.numel() == N * world and torch.equal(full[:N], d_out)
+        res["rccl"] = {"ms": round(el * 1e3, 3), "GBps": round(8 * N * (world - 1) / el / 1e9, 2),
+                       "bytes_moved": 8 * N * (world - 1), "root_check": bool(ok)}
+        del full
+    except Exception as e:
+        res["rccl"] = {"error": str(e)[:200]}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -97,23 +231,41 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--variant", type=int, default=0, help="0 tiled (default), 1 wave-walk")
+    ap.add_argument("--variant", type=int, default=0, help="RLEv2 kernel variant (0 default, 1 wave-walk, ...)")
     ap.add_argument("--copy-inclusive", type=int, default=3,
                     help="steps of the PCIe-inclusive pipeline to time (host bytes -> host values); 0 = skip")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--no-concat", action="store_true", help="skip the N > 1 concat legs")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's RANK / LOCAL_RANK / WORLD_SIZE and exit before touching the GPU")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus}),
+              flush=True)
+        return
 
     import torch
 
-    torch.cuda.set_device(local_rank)
+    # one GPU per rank; on a box with fewer GPUs than ranks (the gloo
+    # rehearsal of the N > 1 path on one GPU) ranks share devices round robin
+    ndev = torch.cuda.device_count()
+    device = local_rank % ndev if ndev else local_rank
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.backend)
+        world = dist.get_world_size()
 
     import orc_amd
 
@@ -123,7 +275,7 @@ def main():
     N = args.rows
 
     stream = torch.cuda.Stream()
-    ctx = orc_amd.Context(local_rank, stream=stream)
+    ctx = orc_amd.Context(device, stream=stream)
     ctx.set_rlev2_variant(args.variant)
     with torch.cuda.stream(stream):
         d_src = torch.from_numpy(data).to("cuda")
@@ -160,6 +312,8 @@ def main():
     e_end.record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     t1 = time.perf_counter()
     ctx.synchronize()  # surfaces any device-side decode error
     elapsed = t1 - t0
@@ -167,7 +321,6 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        dist.barrier()
     kern_ms = e_start.elapsed_time(e_end) / args.steps
     # outside the timed region: the same K launches with an event after each
     # one (per-launch durations, as rocprofv3 --kernel-trace timestamps every
@@ -181,10 +334,14 @@ def main():
     ctx.synchronize()
     per_launch = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
 
+    concat = None
+    if dist and not args.no_concat:
+        concat = concat_legs(dist, d_out, N, world, rank, stream)
+
     copy_incl = None
     if args.copy_inclusive and rank == 0:
         # host stream bytes (pinned) -> H2D -> decode -> D2H into a pinned
-        # host column: the rate a host-memory caller sees (DESIGN.md §5)
+        # host column: the rate a host-memory caller sees (DESIGN.md §4)
         h_src = torch.from_numpy(data).pin_memory()
         h_out = torch.empty(N, dtype=torch.int64).pin_memory()
         ts = []
@@ -199,7 +356,7 @@ def main():
             ts.append(time.perf_counter() - c0)
         t_ci = float(np.median(ts[1:]))
         copy_incl = {"GBps_decoded": round(8 * N / t_ci / 1e9, 2), "ms": round(t_ci * 1e3, 3),
-                     "h2d_bytes": S, "d2h_bytes": 8 * N}
+                     "h2d_bytes": S, "d2h_bytes": 8 * N, "pipeline": "serial (one stream)"}
         if not args.no_verify and not torch.equal(h_out, torch.from_numpy(values)):
             raise SystemExit("copy-inclusive decode mismatch")
 
@@ -232,7 +389,8 @@ def main():
                 "stream_bytes": S,
                 "row_index_stride": args.stride,
                 "parallelism": "stripe-sharded x%d" % world,
-                "kernel": ["rlev2_tiled_kernel", "rlev2_decode_kernel"][args.variant],
+                "kernel": "rlev2_decode_kernel" if args.variant == 1 else "rlev2_tiled_kernel",
+                "variant": args.variant,
             },
             "roofline": {
                 "bound": "hbm",
@@ -248,12 +406,15 @@ def main():
                 "algorithmic_bytes_per_launch": algo_bytes,
             },
         }
+        if concat:
+            line["concat"] = concat
         if copy_incl:
             line["copy_inclusive"] = copy_incl
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(data, N, args.cpu_budget)
         print(json.dumps(line), flush=True)
     if dist:
+        dist.barrier()
         dist.destroy_process_group()
 
 

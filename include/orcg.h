@@ -62,11 +62,20 @@ const char* orcg_ctx_last_error(const orcg_ctx* ctx);
  * LDS; WAVE_WALK is one wavefront per segment reading HBM directly. Both are
  * bit-identical. */
 enum { ORCG_RLEV2_TILED = 0, ORCG_RLEV2_WAVE_WALK = 1 };
+/* Other accepted values pin one instance of the tiled kernel (used by the
+ * parity tests to cover every instance the default may pick, and by A/B
+ * timing); orcg_rlev2_variants lists them. Unknown values: INVALID_ARGUMENT. */
 int orcg_ctx_set_rlev2_variant(orcg_ctx* ctx, int variant);
+/* Writes up to `cap` accepted variant ids to `out`; returns how many exist. */
+int orcg_rlev2_variants(int* out, int cap);
 
 const char* orcg_version(void);
 /* Number of visible HIP devices (0 when none; never aborts). */
 int orcg_device_count(void);
+/* Page-lock / release caller host memory for asynchronous D2H copies (e.g.
+ * each rank's slice of a shared host batch, orc_amd/shard.py). */
+int orcg_host_register(void* host, uint64_t bytes);
+int orcg_host_unregister(void* host);
 
 /* ---- segments: the ORC-native parallel sync points ----------------------
  * A segment is a run-aligned byte offset in an uncompressed (or already

@@ -29,6 +29,7 @@ from .rle import (  # noqa: F401
     encode_runs,
     rlev1_decode,
     rlev2_decode,
+    rlev2_variants,
     scatter_not_null_device,
     timestamp_decode_device,
 )

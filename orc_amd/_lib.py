@@ -53,8 +53,11 @@ SIGNATURES = [
     ("orcg_ctx_synchronize", [vp], i32),
     ("orcg_ctx_last_error", [vp], cp),
     ("orcg_ctx_set_rlev2_variant", [vp, i32], i32),
+    ("orcg_rlev2_variants", [vp, i32], i32),
     ("orcg_version", [], cp),
     ("orcg_device_count", [], i32),
+    ("orcg_host_register", [vp, u64], i32),
+    ("orcg_host_unregister", [vp], i32),
     ("orcg_rlev2_plan_create", [vp, u64, u64, u64, ctypes.POINTER(vp)], i32),
     ("orcg_rlev2_plan_destroy", [vp], None),
     ("orcg_rlev2_plan_values", [vp], u64),

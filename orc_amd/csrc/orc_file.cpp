@@ -220,8 +220,13 @@ struct DynCodecs {
   DynCodecs() {
     if (void* h = dlopen("liblz4.so.1", RTLD_NOW | RTLD_LOCAL)) lz4 = (lz4_fn)dlsym(h, "LZ4_decompress_safe");
     if (void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL)) {
-      zstd = (zstd_fn)dlsym(h, "ZSTD_decompress");
-      zstd_is_error = (zstd_err_fn)dlsym(h, "ZSTD_isError");
+      // usable only when both entry points resolve
+      const zstd_fn d = (zstd_fn)dlsym(h, "ZSTD_decompress");
+      const zstd_err_fn e = (zstd_err_fn)dlsym(h, "ZSTD_isError");
+      if (d && e) {
+        zstd = d;
+        zstd_is_error = e;
+      }
     }
   }
 };
@@ -298,7 +303,7 @@ bool parse_stripe_footer(const uint8_t* p, uint64_t n, uint64_t stripe_offset, S
       }
       if (!s.ok) return false;
       si.offset = off;  // streams are laid out back to back in footer order
-      off += si.length;
+      if (__builtin_add_overflow(off, si.length, &off)) return false;  // lengths past 2^64: corrupt
       sf.streams.push_back(si);
     } else if (f == 2 && w == 2) {
       Pb s = m.bytes();
@@ -331,7 +336,11 @@ bool split_chunks(const uint8_t* file, uint64_t off, uint64_t len, uint32_t comp
     return true;
   }
   uint64_t p = off;
-  const uint64_t end = off + len;
+  uint64_t end;
+  if (__builtin_add_overflow(off, len, &end)) {
+    err = "Read past EOF in DecompressionStream::readBuffer";
+    return false;
+  }
   while (p < end) {
     if (end - p < 3) {
       err = "Read past EOF in DecompressionStream::readBuffer";

@@ -172,6 +172,16 @@ extern "C" {
 
 const char* orcg_version(void) { return "orcg 0.1.0 (gfx950)"; }
 
+int orcg_host_register(void* p, uint64_t bytes) {
+  if (!p || !bytes) return ORCG_INVALID_ARGUMENT;
+  return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? ORCG_OK : ORCG_DEVICE_ERROR;
+}
+
+int orcg_host_unregister(void* p) {
+  if (!p) return ORCG_INVALID_ARGUMENT;
+  return hipHostUnregister(p) == hipSuccess ? ORCG_OK : ORCG_DEVICE_ERROR;
+}
+
 int orcg_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -216,10 +226,20 @@ int orcg_ctx_set_stream(orcg_ctx* c, void* s) {
   return ORCG_OK;
 }
 
+int orcg_rlev2_variants(int* out, int cap) {
+  int n = 0;
+  for (int v = 0; v <= kMaxRlev2Variant; ++v)
+    if (rlev2_variant_valid(v)) {
+      if (out && n < cap) out[n] = v;
+      ++n;
+    }
+  return n;
+}
+
 int orcg_ctx_set_rlev2_variant(orcg_ctx* c, int v) {
-  // 0 tiled (default), 1 wave-walk; 8..19 pin one tiled instance
-  // (rlev2_tiled.hip launch_rlev2_tiled), the others run the default
-  if (!c || v < 0 || v > 20) return ORCG_INVALID_ARGUMENT;
+  // 0 tiled (default), 1 wave-walk; the others pin one tiled instance
+  // (rlev2_tiled.hip launch_rlev2_tiled, rlev2_variant_valid)
+  if (!c || !rlev2_variant_valid(v)) return ORCG_INVALID_ARGUMENT;
   c->rlev2_variant = v;
   return ORCG_OK;
 }

@@ -83,6 +83,10 @@ bool utc_zone(const std::string& z) {
 }
 constexpr int64_t kOrcEpochUtc = 1420070400;
 
+// [off, off + len) lies inside [0, end), written so that no sum can wrap
+// (offsets and lengths come from the file and are untrusted)
+bool range_ok(uint64_t off, uint64_t len, uint64_t end) { return off <= end && len <= end - off; }
+
 // Columns this reader decodes: every primitive, list / map / struct, decimals
 // with a precision (Hive 0.11 precision-0 decimals are not), timestamps of
 // UTC writers. Not: UNION.
@@ -318,14 +322,15 @@ int orcg_reader::open_tail() {
     return fail(ORCG_PARSE_ERROR, "Failed to parse the postscript");
   if (ps.block_size == 0) ps.block_size = 256 * 1024;
   decimal_as_long = ps.version.size() == 2 && ps.version[0] == 1 && ps.version[1] == 9999;
-  const uint64_t tail = 1 + ps_len + ps.footer_length;
-  if (tail >= file_len)
+  // file_len >= 1 + ps_len here, so the subtraction cannot wrap
+  if (ps.footer_length >= file_len - 1 - ps_len)
     return fail(ORCG_PARSE_ERROR, "Invalid tail size: footerSize=" + std::to_string(ps.footer_length) +
                                       ", postscriptLength=" + std::to_string(ps_len) +
                                       ", fileLength=" + std::to_string(file_len));
   if (ps.compression > kZstd) return fail(ORCG_PARSE_ERROR, "Unknown compression type");
   std::vector<uint8_t> fbytes;
   std::string err;
+  const uint64_t tail = 1 + ps_len + ps.footer_length;
   if (!read_range(file, file_len - tail, ps.footer_length, ps.compression, ps.block_size, fbytes, err))
     return fail(ORCG_PARSE_ERROR, err);
   if (!parse_footer(fbytes.data(), fbytes.size(), footer)) return fail(ORCG_PARSE_ERROR, "Failed to parse the footer");
@@ -685,8 +690,11 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   const StripeInfo& si = footer.stripes[s];
   std::string err;
   std::vector<uint8_t> fb;
-  const uint64_t foff = si.offset + si.index_length + si.data_length;
-  if (foff + si.footer_length > file_len) return hs.fail(ORCG_PARSE_ERROR, "stripe footer past the end of the file");
+  // stripe = [offset, + index, + data, + footer), every sum checked
+  uint64_t foff = 0;
+  if (__builtin_add_overflow(si.offset, si.index_length, &foff) ||
+      __builtin_add_overflow(foff, si.data_length, &foff) || !range_ok(foff, si.footer_length, file_len))
+    return hs.fail(ORCG_PARSE_ERROR, "stripe footer past the end of the file");
   if (!read_range(file, foff, si.footer_length, ps.compression, ps.block_size, fb, err))
     return hs.fail(ORCG_PARSE_ERROR, err);
   StripeFooter sf;
@@ -712,16 +720,16 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   };
   std::vector<int> row_index(nt, -1);  // ROW_INDEX stream of each column (index into sf.streams)
   std::vector<Need> needs;
-  const uint64_t data_end = si.offset + si.index_length + si.data_length;
+  const uint64_t data_end = foff;  // <= file_len (checked above)
   for (size_t i = 0; i < sf.streams.size(); ++i) {
     const StreamInfo& st = sf.streams[i];
-    if (st.kind == kRowIndex && st.column < nt && selected[st.column] && hs.cols[st.column].supported &&
-        st.offset + st.length <= data_end)
+    const bool in_stripe = st.offset >= si.offset && range_ok(st.offset, st.length, data_end);
+    if (st.kind == kRowIndex && st.column < nt && selected[st.column] && hs.cols[st.column].supported && in_stripe)
       row_index[st.column] = (int)i;
     const int slot = slot_of(st.kind);
     if (slot < 0 || st.column >= nt) continue;
     if (!selected[st.column] || !hs.cols[st.column].supported) continue;
-    if (st.offset + st.length > data_end)
+    if (!in_stripe)
       return hs.fail(ORCG_PARSE_ERROR, "Malformed stream meta at stream index " + std::to_string(i) + " in stripe " +
                                            std::to_string(s));
     Need nd{st.column, slot, {}, st.offset};

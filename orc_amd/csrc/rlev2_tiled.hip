@@ -1133,7 +1133,9 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
 
 }  // namespace
 
-// Variants (ctx->rlev2_variant): 0 = default; 2.. = tuning experiments.
+bool rlev2_variant_valid(int v) { return v == 0 || v == 1 || (v >= 8 && v <= kMaxRlev2Variant); }
+
+// Variants (ctx->rlev2_variant): 0 = default; 8.. = single instances.
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,

@@ -140,6 +140,16 @@ class RleDecoderV2:
             pass
 
 
+def rlev2_variants():
+    """RLEv2 kernel variants the library accepts (Context.set_rlev2_variant):
+    0 = default, 1 = wave-walk, the rest pin one tiled instance."""
+    L = _lib.load()
+    n = L.orcg_rlev2_variants(None, 0)
+    out = (ctypes.c_int * max(n, 1))()
+    L.orcg_rlev2_variants(out, n)
+    return list(out[:n])
+
+
 def create_rle_decoder(data, is_signed, version=RleVersion_2, ctx=None):
     """createRleDecoder (c++/src/RLE.cc:48-60)."""
     if version != RleVersion_2:

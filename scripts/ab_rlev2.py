@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--stride", type=int, default=10_000)
-    ap.add_argument("--data", default="random", choices=["random", "delta", "repeat", "patched"])
+    ap.add_argument("--data", default="random", choices=["random", "delta", "repeat", "patched", "shortdirect", "shortmix"])
     ap.add_argument("--refs", default="copy,probe2,probe5,probe7,probe11",
                     help="reference copies timed beside the decoder (copy = torch, probeN = orcg_probe_copy mode N)")
     ap.add_argument("--timing-only", default="", help="variants timed even when their output mismatches (debug instances)")
@@ -53,7 +53,32 @@ def main():
                 lens = lens[:-1]
                 n = int(lens.sum())
             kinds = np.zeros(lens.size, dtype=np.uint8)
-            v = np.repeat(rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=lens.size), lens)
+            v = np.repeat(rng.integers(-(1 << (args.bits - 1)), (1 << (args.bits - 1)) - 1, size=lens.size,
+                                       dtype=np.int64, endpoint=True), lens)
+        elif args.data == "shortdirect":
+            # short DIRECT runs (1-10 values) of --bits-wide values: the shape
+            # a writer emits between repeats of a high-cardinality column
+            lens = rng.integers(1, 11, size=n // 5 + 16).astype(np.uint32)
+            lens = lens[: np.searchsorted(np.cumsum(lens), n)]
+            kinds = np.ones(lens.size, dtype=np.uint8)
+            n = int(lens.sum())
+            if args.bits == 64:
+                v = rng.integers(-(1 << 63), (1 << 63) - 1, size=n, dtype=np.int64, endpoint=True)
+            else:
+                v = rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=n, dtype=np.int64)
+        elif args.data == "shortmix":
+            # alternating SHORT_REPEAT (3-10) and short DIRECT (1-10) runs
+            nr = n // 6 + 16
+            kinds = (np.arange(nr) % 2).astype(np.uint8)
+            lens = np.where(kinds == 0, rng.integers(3, 11, size=nr), rng.integers(1, 11, size=nr)).astype(np.uint32)
+            cut = np.searchsorted(np.cumsum(lens), n)
+            lens, kinds = lens[:cut], kinds[:cut]
+            n = int(lens.sum())
+            lo, hi = -(1 << (args.bits - 1)), (1 << (args.bits - 1)) - 1
+            rv = rng.integers(lo, hi, size=lens.size, dtype=np.int64, endpoint=True)
+            v = np.repeat(rv, lens)
+            dmask = np.repeat(kinds == 1, lens)
+            v[dmask] = rng.integers(lo, hi, size=int(dmask.sum()), dtype=np.int64, endpoint=True)
         else:
             lens = np.full(n // 512, 512, dtype=np.uint32)
             kinds = np.full(lens.size, 2, dtype=np.uint8)

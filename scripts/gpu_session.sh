@@ -30,6 +30,15 @@ for s in $STEPS; do
       for b in 1 8 13 24 32 48 64; do run sweep_w$b 300 python scripts/ab_rlev2.py --bits $b --variants 0,1,8,9,10,11,14,15,16,18,19 --rounds 3 || true; done
       for d in delta repeat patched; do run sweep_$d 300 python scripts/ab_rlev2.py --data $d --bits 12 --variants 0,1,8,9,10,11,14,15,16,18,19 --rounds 3 || true; done
       run sweep_repeat40 300 python scripts/ab_rlev2.py --data repeat --bits 40 --variants 0,1,8,9,10,11,14,15,16,18,19 --rounds 3 || true ;;
+    cliff)
+      # short-run shapes at >= 1.25 B/value (the density rule's serial instances) and wide SHORT_REPEAT
+      V=${CLIFF_VARIANTS:-0,8,10,11,15,16,19,20}
+      run cliff_repeat64 300 python scripts/ab_rlev2.py --data repeat --bits 64 --variants $V --rounds 3 --refs probe5 || true
+      run cliff_repeat40 300 python scripts/ab_rlev2.py --data repeat --bits 40 --variants $V --rounds 3 --refs probe5 || true
+      run cliff_repeat12 300 python scripts/ab_rlev2.py --data repeat --bits 12 --variants $V --rounds 3 --refs probe5 || true
+      run cliff_sdir16 300 python scripts/ab_rlev2.py --data shortdirect --bits 16 --variants $V --rounds 3 --refs probe5 || true
+      run cliff_sdir64 300 python scripts/ab_rlev2.py --data shortdirect --bits 64 --variants $V --rounds 3 --refs probe5 || true
+      run cliff_smix32 300 python scripts/ab_rlev2.py --data shortmix --bits 32 --variants $V --rounds 3 --refs probe5 || true ;;
     benchwalk) run bench_walk 600 python bench.py --variant 1 --no-cpu-baseline ;;
     prof)
       export TMPDIR=/tmp

@@ -157,3 +157,26 @@ def test_file_without_row_index_uses_host_plans(ctx):
     r.read_stripe(0)
     st = r.last_stream_stats()
     assert st["row_index"] == 0 and st["host_plan"] > 0
+
+
+def test_crafted_offsets_that_wrap_are_rejected(ctx):
+    """Stripe offsets / lengths near 2^64 must fail the bounds checks instead
+    of wrapping past them (the reference's InputStream reads are bounds
+    checked; here every sum over file-supplied sizes is checked)."""
+    from orc_craft import field_bytes, field_varint, orc_file, stripe_info, type_msg
+
+    types = [type_msg(12, [1], ["x"]), type_msg(4)]
+    # stripe footer at offset + index + data that wraps around 2^64
+    wrap = orc_file(b"", [stripe_info((1 << 64) - 16, 8, 8, 4, 1)], types, 1)
+    r = orc_amd.Reader(wrap, ctx)
+    with pytest.raises(orc_amd.ParseError, match="stripe footer past the end of the file"):
+        r.read_stripe(0)
+    # a stream whose length wraps the running stream offset
+    sfoot = (field_bytes(1, field_varint(1, 1) + field_varint(2, 1) + field_varint(3, (1 << 64) - 2)) +
+             field_bytes(1, field_varint(1, 1) + field_varint(2, 1) + field_varint(3, 16)) +
+             field_bytes(2, field_varint(1, 0)) + field_bytes(2, field_varint(1, 0)))
+    body = bytes(8) + sfoot
+    bad = orc_file(body, [stripe_info(3, 0, 8, len(sfoot), 1)], types, 1)
+    r = orc_amd.Reader(bad, ctx)
+    with pytest.raises(orc_amd.ParseError):
+        r.read_stripe(0)

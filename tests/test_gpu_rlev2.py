@@ -212,6 +212,23 @@ def _stream_with_positions(orc, rng, kind, n, stride, bits=12):
             base = int(rng.integers(-(1 << 40), 1 << 40))
             out.append(base + s * np.cumsum(rng.integers(1, 1 << bits, size=int(L))))
         v = np.concatenate(out)
+    elif kind == "wide":
+        # >= 5 stream bytes per value, so variant 0 picks the 33 KB
+        # register-fill instance with the full-run fast paths: DIRECT runs of
+        # 47-bit values alternating with DELTA runs of 40-bit deltas, some
+        # ragged (300 values)
+        lens = np.full(n // 512, 512, dtype=np.uint32)
+        lens[::5] = 300
+        kinds = np.where(np.arange(lens.size) % 2 == 0, 1, 3).astype(np.uint8)
+        out = []
+        for L, k in zip(lens, kinds):
+            if k == 1:
+                out.append(rng.integers(-(1 << 46), 1 << 46, size=int(L)))
+            else:
+                s = 1 if rng.integers(0, 2) else -1
+                base = int(rng.integers(-(1 << 50), 1 << 50))
+                out.append(base + s * np.cumsum(rng.integers(1 << 38, 1 << 40, size=int(L))))
+        v = np.concatenate(out)
     else:  # patched
         lens = np.full(n // 512, 512, dtype=np.uint32)
         kinds = np.full(lens.size, 2, dtype=np.uint8)
@@ -230,7 +247,7 @@ def _stream_with_positions(orc, rng, kind, n, stride, bits=12):
     return v, data, pos
 
 
-@pytest.mark.parametrize("kind", ["repeat", "delta", "patched"])
+@pytest.mark.parametrize("kind", ["repeat", "delta", "patched", "wide"])
 def test_structured_streams_every_variant(kind):
     """Every kernel variant (ORCG_RLEV2_* and the tuning variants) is
     bit-exact on SR-heavy (run tables that fill up), DELTA-heavy and
@@ -239,15 +256,17 @@ def test_structured_streams_every_variant(kind):
 
     import orc_amd
 
-    rng = np.random.default_rng({"repeat": 1, "delta": 2, "patched": 3}[kind])
+    rng = np.random.default_rng({"repeat": 1, "delta": 2, "patched": 3, "wide": 4}[kind])
     ctx = orc_amd.default_context(0)
     for stride in (10_000, 1 << 30):
         v, data, pos = _stream_with_positions(orc_amd, rng, kind, 300_000, stride)
         want = oracle.rlev2_decode(data.tobytes(), v.size, True)
         np.testing.assert_array_equal(want, v)
+        if kind == "wide":
+            assert data.size >= 5 * v.size  # reaches the >= 5 B/value default instance
         d_src = torch.from_numpy(data).cuda()
         d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
-        for variant in range(20):
+        for variant in orc_amd.rlev2_variants():
             ctx.set_rlev2_variant(variant)
             out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
             orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, True, out)

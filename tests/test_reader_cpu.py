@@ -78,3 +78,16 @@ def test_checker_pinned_to_reference_expected_output(name):
 def test_corrupt_fixtures_present():
     for name, _ in CORRUPT_FILES:
         assert os.path.exists(path(name))
+
+
+def test_tail_with_wrapping_footer_length_is_rejected():
+    """A PostScript footer length near 2^64 must not wrap the tail-size check
+    (Reader.cc readPostscript / the tail bounds)."""
+    from orc_craft import orc_file, type_msg
+
+    good = orc_file(b"", [], [type_msg(12)], 0)
+    assert orc_amd.Reader(good).num_rows == 0
+    for flen in ((1 << 64) - 1, (1 << 64) - 5, 1 << 63, 10 ** 9):
+        bad = orc_file(b"", [], [type_msg(12)], 0, footer_length_override=flen)
+        with pytest.raises(orc_amd.ParseError, match="Invalid tail size"):
+            orc_amd.Reader(bad)

@@ -89,3 +89,79 @@ def test_gloo_world2_sharded_decode_matches_pyarrow(tmp_path):
     full, path = _run(tmp_path, use_gpu=True)
     want = pa.ORCFile(path).read(columns=["_col0"]).column(0).to_numpy(zero_copy_only=False)
     np.testing.assert_array_equal(full, want.astype(np.int64))
+
+
+def _host_concat_worker(rank, world, port, path, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    from orc_amd.shard import write_rows_to_shared_host
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # ragged shards (rank r holds 1000 + 37 r rows, rank 2 of 3 none)
+        n = 0 if (world == 3 and rank == 2) else 1000 + 37 * rank
+        start = sum(0 if (world == 3 and q == 2) else 1000 + 37 * q for q in range(rank))
+        local = torch.arange(start, start + n, dtype=torch.int64)
+        host = write_rows_to_shared_host(dist, local, path, create=(rank == 0))
+        if rank == 0:
+            np.save(os.path.join(out_dir, "host.npy"), host.numpy().copy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_concat_into_shared_host_batch(tmp_path, world):
+    """DESIGN §5 option 2: each rank writes its rows into its own slice of one
+    shared host batch (offsets from an all-gather of counts), no data
+    collective."""
+    shm = os.path.join(str(tmp_path), "batch.bin")
+    mp.start_processes(_host_concat_worker, args=(world, _free_port(), shm, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    got = np.load(os.path.join(tmp_path, "host.npy"))
+    n = sum(0 if (world == 3 and q == 2) else 1000 + 37 * q for q in range(world))
+    np.testing.assert_array_equal(got, np.arange(n))
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` starts two ranks itself (torch.distributed.run as a
+    child, before any GPU use); --dry-run makes each rank report its
+    environment and exit."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert sorted((d["rank"], d["local_rank"], d["world_size"]) for d in lines) == [(0, 0, 2), (1, 1, 2)]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu_with_gloo():
+    """The N > 1 bench path end to end on one GPU (both ranks share cuda:0;
+    gloo instead of RCCL, which needs one GPU per rank): per-rank decode,
+    max-over-ranks timing, the shared-host concat; one JSON line from rank 0."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                          "--rows", "2000000", "--steps", "3", "--warmup", "2", "--no-cpu-baseline",
+                          "--copy-inclusive", "0"], capture_output=True, text=True, timeout=240, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "ms" in d["concat"]["host"], d["concat"]
