@@ -169,6 +169,11 @@ int orcg_rle_decoder_seek(orcg_rle_decoder* dec, const uint64_t* positions, uint
  * be NULL (no nulls). */
 int orcg_rle_decoder_next_vector_java(orcg_rle_decoder* dec, int64_t* vector, const uint8_t* is_null,
                                       uint64_t n, int* is_repeating);
+/* The int[] overload (RunLengthIntegerReaderV2.java:399-411): values narrowed
+ * to int32 ((int) next()), null slots 1; with a null mask, a vector that is
+ * repeating with isNull[0] is left untouched; isRepeating is an input only. */
+int orcg_rle_decoder_next_vector_java_int(orcg_rle_decoder* dec, int32_t* vector, const uint8_t* is_null, uint64_t n,
+                                          int is_repeating);
 const char* orcg_rle_decoder_last_error(const orcg_rle_decoder* dec);
 
 /* ---- byte RLE / boolean RLE (PRESENT, BOOLEAN, BYTE streams) -------------

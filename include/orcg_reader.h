@@ -29,10 +29,17 @@
  *   LIST, MAP                             : int64 offsets[n + 1] (ListVectorBatch::offsets);
  *                                           children hold offsets[n] rows
  *   STRUCT                                : not_null only; children hold n rows
+ *   UNION                                 : uint8 tags[n], int64 offsets[n] (UnionVectorBatch::tags /
+ *                                           offsets: the row's index in child tags[i])
+ * Dictionary-encoded strings also expose int64 index[n] (the entry of each
+ * row, EncodedStringVectorBatch::index) and int64 dict_offsets[dict_size + 1]
+ * into blob (StringDictionary::dictionaryOffset); with lazy dictionary
+ * decoding (orcg_reader_set_lazy_dictionary, RowReaderOptions::
+ * setEnableLazyDecoding) only those are produced (data / length are NULL).
  * Null slots hold 0 (the reference leaves them unspecified). Not decoded
- * (view.decoded == 0): UNION columns, Hive 0.11 decimals (precision 0) and
- * TIMESTAMP columns whose writer time zone is not UTC (the reference converts
- * those with the IANA zone rules, Timezone.cc).
+ * (view.decoded == 0): Hive 0.11 decimals (precision 0) and TIMESTAMP columns
+ * whose writer time zone is not UTC (the reference converts those with the
+ * IANA zone rules, Timezone.cc).
  */
 #ifndef ORCG_READER_H
 #define ORCG_READER_H
@@ -83,6 +90,10 @@ typedef struct {
   const uint8_t* blob;     /* device: string bytes */
   uint64_t blob_len;
   const int64_t* secondary; /* device: TIMESTAMP nanoseconds (TimestampVectorBatch::nanoseconds) */
+  const uint8_t* tags;      /* device: UNION child per row */
+  const int64_t* index;     /* device: dictionary entry per row (dictionary-encoded strings) */
+  const int64_t* dict_offsets; /* device: dict_size + 1 entry offsets into blob */
+  uint64_t dict_size;
 } orcg_column_view;
 
 /* Open an ORC file held in host memory (the caller keeps `file` alive until
@@ -105,6 +116,16 @@ uint64_t orcg_reader_compression_block_size(const orcg_reader* r);
 /* file version [major, minor] (PostScript.version) */
 int orcg_reader_format_version(const orcg_reader* r, uint32_t* major, uint32_t* minor);
 uint32_t orcg_reader_writer_version(const orcg_reader* r);
+/* Footer.contentLength (Reader::getContentLength, Reader.cc:755) */
+uint64_t orcg_reader_content_length(const orcg_reader* r);
+/* Reader::getSoftwareVersion (Reader.cc:742-749): writer id name, then the
+ * footer's softwareVersion when present ("ORC Java", "ORC C++ 1.8.0", ...) */
+const char* orcg_reader_software_version(const orcg_reader* r);
+/* User metadata (Reader::getMetadataKeys / getMetadataValue, Reader.cc:783-798):
+ * key i and its value bytes (NULL past the end). */
+uint32_t orcg_reader_num_metadata(const orcg_reader* r);
+const char* orcg_reader_metadata_key(const orcg_reader* r, uint32_t i);
+const uint8_t* orcg_reader_metadata_value(const orcg_reader* r, uint32_t i, uint64_t* len);
 uint32_t orcg_reader_num_types(const orcg_reader* r);
 int orcg_reader_type(const orcg_reader* r, uint32_t type_id, orcg_type_info* out);
 int orcg_reader_subtypes(const orcg_reader* r, uint32_t type_id, uint32_t* out, uint32_t cap);
@@ -114,6 +135,11 @@ int orcg_reader_stripe(const orcg_reader* r, uint64_t stripe, orcg_stripe_info* 
 /* Column selection by type id (RowReaderOptions::include; NULL = all). A
  * selected column's ancestors are read too. */
 int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes);
+/* 1 if the type id is read under the current selection (RowReader::getSelectedColumns) */
+int orcg_reader_is_selected(const orcg_reader* r, uint32_t type_id);
+/* RowReaderOptions::setEnableLazyDecoding: dictionary string columns decode to
+ * index + dictionary only (StringDictionaryColumnReader::nextEncoded). */
+int orcg_reader_set_lazy_dictionary(orcg_reader* r, int on);
 
 /* Decode one stripe of the selected columns into device batches owned by the
  * reader (valid until the next read or destroy). Synchronous. */
@@ -124,6 +150,33 @@ int orcg_reader_column(const orcg_reader* r, uint32_t type_id, orcg_column_view*
  * decodes stripe i. orcg_reader_stripe_column(r, k, ...) views the k-th. */
 int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count);
 int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t type_id, orcg_column_view* out);
+
+/* ---- RowReader (c++/include/orc/Reader.hh:640-790; c++/src/Reader.cc
+ * RowReaderImpl) over the GPU stripe decode. Batches hold at most `capacity`
+ * rows and never span two stripes (RowReaderImpl::next, Reader.cc:1402-1403).
+ * Each batch is a row range of the stripe decoded in HBM; per column,
+ * orcg_row_reader_column gives the stripe's column view plus the element
+ * range [begin, begin + count) of the batch (through list / map offsets and
+ * union tags), which host adapters copy out. The row reader borrows the
+ * reader (and its column selection and stripe slot 0). */
+typedef struct orcg_row_reader orcg_row_reader;
+typedef struct {
+  uint64_t offset, length;   /* RowReaderOptions::range: stripes whose offset lies in [offset, offset + length) */
+  const uint8_t* include;    /* RowReaderOptions::include by type id (NULL = every column) */
+  uint32_t include_len;
+  int lazy_dictionary;       /* RowReaderOptions::setEnableLazyDecoding */
+} orcg_row_reader_options;
+/* opts NULL = the whole file, every column */
+int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* opts, orcg_row_reader** out);
+void orcg_row_reader_destroy(orcg_row_reader* rr);
+/* RowReader::next: *rows = rows in the new batch (0 at the end) */
+int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows);
+/* RowReader::getRowNumber: first row of the last batch (UINT64_MAX before the first) */
+uint64_t orcg_row_reader_row_number(const orcg_row_reader* rr);
+/* RowReader::seekToRow: the next batch starts at `row` */
+int orcg_row_reader_seek_to_row(orcg_row_reader* rr, uint64_t row);
+int orcg_row_reader_column(const orcg_row_reader* rr, uint32_t type_id, orcg_column_view* view, uint64_t* begin,
+                           uint64_t* count);
 
 /* Device -> host copy on the reader's context stream (synchronous). */
 int orcg_reader_copy_to_host(orcg_reader* r, void* host_dst, const void* device_src, uint64_t bytes);

@@ -34,6 +34,6 @@ from .rle import (  # noqa: F401
     timestamp_decode_device,
 )
 
-from .reader import Reader, open_reader  # noqa: F401,E402
+from .reader import Reader, RowReader, UnionValue, open_reader  # noqa: F401,E402
 
 __version__ = "0.1.0"

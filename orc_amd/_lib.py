@@ -76,6 +76,7 @@ SIGNATURES = [
     ("orcg_rle_decoder_skip", [vp, u64], i32),
     ("orcg_rle_decoder_seek", [vp, vp, u64], i32),
     ("orcg_rle_decoder_next_vector_java", [vp, vp, vp, u64, ctypes.POINTER(i32)], i32),
+    ("orcg_rle_decoder_next_vector_java_int", [vp, vp, vp, u64, i32], i32),
     ("orcg_rle_decoder_last_error", [vp], cp),
     ("orcg_rlev1_plan_create", [vp, u64, u64, u64, ctypes.POINTER(vp)], i32),
     ("orcg_rlev1_decode_device", [vp, vp, u64, i32, vp, u64, u64, u64, vp, i32], i32),
@@ -119,7 +120,12 @@ class ColumnView(ctypes.Structure):
     _fields_ = [("type_id", ctypes.c_uint32), ("kind", ctypes.c_uint32), ("encoding", ctypes.c_uint32),
                 ("decoded", ctypes.c_uint32), ("num_elements", u64), ("has_nulls", i32), ("not_null", vp),
                 ("data", vp), ("length", vp), ("offsets", vp), ("blob", vp), ("blob_len", u64),
-                ("secondary", vp)]
+                ("secondary", vp), ("tags", vp), ("index", vp), ("dict_offsets", vp), ("dict_size", u64)]
+
+
+class RowReaderOptions(ctypes.Structure):
+    _fields_ = [("offset", u64), ("length", u64), ("include", vp), ("include_len", ctypes.c_uint32),
+                ("lazy_dictionary", i32)]
 
 
 u32 = ctypes.c_uint32
@@ -150,6 +156,20 @@ SIGNATURES += [
     ("orcg_reader_copy_to_host", [vp, vp, vp, u64], i32),
     ("orcg_reader_last_timings", [vp, ctypes.POINTER(ctypes.c_double)], i32),
     ("orcg_reader_last_stream_stats", [vp, ctypes.POINTER(u64)], i32),
+    ("orcg_reader_content_length", [vp], u64),
+    ("orcg_reader_software_version", [vp], cp),
+    ("orcg_reader_num_metadata", [vp], u32),
+    ("orcg_reader_metadata_key", [vp, u32], cp),
+    ("orcg_reader_metadata_value", [vp, u32, ctypes.POINTER(u64)], vp),
+    ("orcg_reader_set_lazy_dictionary", [vp, i32], i32),
+    ("orcg_reader_is_selected", [vp, u32], i32),
+    ("orcg_row_reader_create", [vp, ctypes.POINTER(RowReaderOptions), ctypes.POINTER(vp)], i32),
+    ("orcg_row_reader_destroy", [vp], None),
+    ("orcg_row_reader_next", [vp, u64, ctypes.POINTER(u64)], i32),
+    ("orcg_row_reader_row_number", [vp], u64),
+    ("orcg_row_reader_seek_to_row", [vp, u64], i32),
+    ("orcg_row_reader_column", [vp, u32, ctypes.POINTER(ColumnView), ctypes.POINTER(u64), ctypes.POINTER(u64)],
+     i32),
 ]
 
 

@@ -296,6 +296,42 @@ __global__ void rg_child_rows_kernel(const int64_t* __restrict__ offsets, const 
   if (g < G) out[g] = offsets[rows[g]];
 }
 
+// ---- UNION (UnionColumnReader, c++/src/ColumnReader.cc:1158-1274) ----
+// tags[j] (byte RLE DATA, one per non-null row) select the child; a row's
+// offset is its rank among the rows with the same tag. flags[j] = tags[j] ==
+// k feeds an exclusive scan per child; the first tag >= nchildren (lowest
+// index) is kept as (index << 8 | tag) for getCheckedUnionTag's message.
+__global__ void union_flags_kernel(const uint8_t* __restrict__ tags, uint64_t n, uint32_t k,
+                                   int64_t* __restrict__ flags) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    flags[i] = tags[i] == k ? 1 : 0;
+}
+
+__global__ void union_check_kernel(const uint8_t* __restrict__ tags, uint64_t n, uint32_t nchildren,
+                                   unsigned long long* first_bad) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long best = ~0ull;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    if (tags[i] >= nchildren) {
+      best = (unsigned long long)i << 8 | tags[i];
+      break;  // later rows of this thread cannot be earlier
+    }
+  for (int m = 32; m >= 1; m >>= 1) {
+    const unsigned long long o = __shfl_xor(best, m);
+    best = o < best ? o : best;
+  }
+  if ((threadIdx.x % kWave) == 0 && best != ~0ull) atomicMin(first_bad, best);
+}
+
+// offsets[j] = scan_k[j] for the rows with tag k
+__global__ void union_offsets_kernel(const uint8_t* __restrict__ tags, uint64_t n, uint32_t k,
+                                     const int64_t* __restrict__ scan_k, int64_t* __restrict__ offsets) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    if (tags[i] == k) offsets[i] = scan_k[i];
+}
+
 }  // namespace
 
 // 16-byte elements (Decimal128 values, orc::Int128 layout [hi, lo])
@@ -456,6 +492,31 @@ int launch_rg_child_rows(Ctx* ctx, const int64_t* d_offsets, const int64_t* d_ro
   hipLaunchKernelGGL(rg_child_rows_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, ctx->stream, d_offsets,
                      d_rows, G, d_out);
   return hip_check(ctx, hipGetLastError(), "rg_child_rows_kernel launch");
+}
+
+int launch_union_flags(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t k, int64_t* d_flags) {
+  if (n == 0) return ORCG_OK;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(union_flags_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_tags, n, k, d_flags);
+  return hip_check(ctx, hipGetLastError(), "union_flags_kernel launch");
+}
+
+int launch_union_check(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t nchildren, uint64_t* d_first_bad) {
+  int rc = hip_check(ctx, hipMemsetAsync(d_first_bad, 0xff, sizeof(uint64_t), ctx->stream), "union memset");
+  if (rc || n == 0) return rc;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(union_check_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_tags, n, nchildren,
+                     (unsigned long long*)d_first_bad);
+  return hip_check(ctx, hipGetLastError(), "union_check_kernel launch");
+}
+
+int launch_union_offsets(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t k, const int64_t* d_scan_k,
+                         int64_t* d_offsets) {
+  if (n == 0) return ORCG_OK;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(union_offsets_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_tags, n, k, d_scan_k,
+                     d_offsets);
+  return hip_check(ctx, hipGetLastError(), "union_offsets_kernel launch");
 }
 
 }  // namespace orcg

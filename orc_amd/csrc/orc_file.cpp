@@ -205,6 +205,126 @@ bool snappy_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap
   return true;
 }
 
+// ---- LZO1X (the reference implements it itself: c++/src/LzoDecompressor.cc) --
+// An LZO1X block is a sequence of instructions. A literal run copies bytes
+// from the input; a match copies `len` bytes from `dist` back in the output
+// (overlapping copies repeat). Every match carries, in the low two bits of
+// its last distance byte, the count (0-3) of literals that follow it.
+//   first byte > 17      : literal run of (byte - 17), then state "after literals"
+//   0000LLLL             : literal run of L + 3 (L = 0: 15 + 255 per zero byte + next)
+//   after a run, 0000DDSS: 3-byte match, dist = 1 + 0x800 + (D | next << 2)
+//   after a match, 0000DDSS: 2-byte match, dist = 1 + (D | next << 2)
+//   LLLDDDSS (>= 64)     : match of L + 1 bytes, dist = 1 + (D | next << 3)
+//   001LLLLL (32..63)    : match of L + 2 (L = 0: 31 + 255 per zero + next), dist = 1 + (u16le >> 2)
+//   0001HLLL (16..31)    : match of L + 2 (L = 0: 7 + ...), dist = 0x4000 + (H << 14) + (u16le >> 2);
+//                          distance 0x4000 exactly ends the block
+namespace {
+
+bool lzo_decompress(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap, uint64_t& out_len,
+                    std::string& err) {
+  const uint8_t* ip = in;
+  const uint8_t* const ie = in + n;
+  uint64_t op = 0;
+  auto fail = [&](const char* m) {
+    err = std::string("LZO: ") + m;
+    return false;
+  };
+  auto literals = [&](uint64_t t) -> bool {
+    if ((uint64_t)(ie - ip) < t) return false;
+    if (cap - op < t) return false;
+    memcpy(out + op, ip, t);
+    ip += t;
+    op += t;
+    return true;
+  };
+  auto copy_match = [&](uint64_t dist, uint64_t len) -> bool {
+    if (dist == 0 || dist > op || cap - op < len) return false;
+    const uint64_t from = op - dist;
+    for (uint64_t k = 0; k < len; ++k) out[op + k] = out[from + k];  // may overlap forward
+    op += len;
+    return true;
+  };
+  auto long_length = [&](uint64_t base, uint64_t& t) -> bool {
+    // t == 0: 255 per zero byte, then base + the next byte
+    while (true) {
+      if (ip >= ie) return false;
+      if (*ip != 0) break;
+      t += 255;
+      ++ip;
+    }
+    t += base + *ip++;
+    return true;
+  };
+  if (ip >= ie) return fail("empty input");
+  // state: 0 = expecting an instruction after a match with no trailing
+  // literals, 1 = right after a literal run of >= 4 bytes, 2 = right after
+  // a match with 1-3 trailing literals
+  int state = 0;
+  uint64_t t = 0;
+  if (*ip > 17) {
+    t = *ip++ - 17u;
+    if (!literals(t)) return fail("literal run past the end");
+    state = t < 4 ? 2 : 1;
+  }
+  while (true) {
+    if (ip >= ie) return fail("truncated input");
+    t = *ip++;
+    uint64_t len = 0, dist = 0;
+    if (t < 16) {
+      if (state == 0) {
+        // literal run
+        if (t == 0 && !long_length(15, t)) return fail("truncated run length");
+        if (!literals(t + 3)) return fail("literal run past the end");
+        state = 1;
+        continue;
+      }
+      if (ip >= ie) return fail("truncated match");
+      dist = 1 + (t >> 2) + ((uint64_t)*ip++ << 2);
+      if (state == 1) {
+        dist += 0x800;
+        len = 3;
+      } else {
+        len = 2;
+      }
+    } else if (t >= 64) {
+      if (ip >= ie) return fail("truncated match");
+      dist = 1 + ((t >> 2) & 7u) + ((uint64_t)*ip++ << 3);
+      len = (t >> 5) + 1;
+    } else if (t >= 32) {
+      len = t & 31u;
+      if (len == 0 && !long_length(31, len)) return fail("truncated match length");
+      len += 2;
+      if (ie - ip < 2) return fail("truncated match");
+      dist = 1 + ((ip[0] >> 2) | ((uint64_t)ip[1] << 6));
+      ip += 2;
+    } else {
+      len = t & 7u;
+      if (len == 0 && !long_length(7, len)) return fail("truncated match length");
+      len += 2;
+      if (ie - ip < 2) return fail("truncated match");
+      dist = ((uint64_t)(t & 8u) << 11) + ((ip[0] >> 2) | ((uint64_t)ip[1] << 6));
+      ip += 2;
+      if (dist == 0) {  // the end-of-stream marker
+        if (ip != ie) return fail("data after the end of the block");
+        out_len = op;
+        return true;
+      }
+      dist += 0x4000;
+    }
+    if (!copy_match(dist, len)) return fail("match outside the output");
+    // trailing literals: the low two bits of the last distance byte read
+    const uint64_t lit = ip[-2] & 3u;
+    if (lit) {
+      if (!literals(lit)) return fail("literal run past the end");
+      state = 2;
+    } else {
+      state = 0;
+    }
+  }
+}
+
+}  // namespace
+
 // ---- lz4 / zstd through the system libraries (dlopen) ----------------------
 // The reference links liblz4 (LZ4_decompress_safe, Compression.cc Lz4
 // DecompressionStream) and libzstd (ZSTD_decompressDCtx). Only the runtime
@@ -281,7 +401,22 @@ bool parse_footer(const uint8_t* p, uint64_t n, Footer& ft) {
     } else if (f == 6 && w == 0) ft.num_rows = m.varint();
     else if (f == 8 && w == 0) ft.row_index_stride = (uint32_t)m.varint();
     else if (f == 9 && w == 0) ft.writer = (uint32_t)m.varint();
-    else m.skip(w);
+    else if (f == 12 && w == 2) {
+      ft.has_software_version = true;
+      ft.software_version = m.str();
+    } else if (f == 5 && w == 2) {
+      // UserMetadataItem {name = 1, value = 2}
+      Pb u = m.bytes();
+      std::string name, value;
+      uint32_t g, v;
+      while (u.more() && u.key(g, v)) {
+        if (g == 1 && v == 2) name = u.str();
+        else if (g == 2 && v == 2) value = u.str();
+        else u.skip(v);
+      }
+      if (!u.ok) return false;
+      ft.metadata.emplace_back(std::move(name), std::move(value));
+    } else m.skip(w);
   }
   return m.ok;
 }
@@ -409,8 +544,7 @@ bool decompress_chunk(uint32_t compression, const uint8_t* file, Chunk& c, uint8
       return true;
     }
     case kLzo:
-      err = "LZO compression is not supported by the GPU reader";
-      return false;
+      return lzo_decompress(in, c.src_len, dst, cap, c.dst_len, err);
   }
   err = "Unknown compression type";
   return false;

@@ -47,7 +47,10 @@ struct Footer {
   std::vector<StripeInfo> stripes;
   std::vector<TypeInfo> types;
   uint32_t row_index_stride = 0;
-  uint32_t writer = 0;
+  uint32_t writer = 0;          // Footer.writer (WriterId), ORC Java when absent
+  bool has_software_version = false;
+  std::string software_version;  // Footer.softwareVersion
+  std::vector<std::pair<std::string, std::string>> metadata;  // Footer.metadata (UserMetadataItem name, value)
 };
 
 enum StreamKind {

@@ -543,6 +543,23 @@ int orcg_rle_decoder_next_vector_java(orcg_rle_decoder* d, int64_t* vector, cons
   return ORCG_OK;
 }
 
+int orcg_rle_decoder_next_vector_java_int(orcg_rle_decoder* d, int32_t* vector, const uint8_t* is_null, uint64_t n,
+                                          int is_repeating) {
+  if (!d || (n && !vector)) return ORCG_INVALID_ARGUMENT;
+  // RunLengthIntegerReaderV2.nextVector(ColumnVector, int[], int)
+  // (RunLengthIntegerReaderV2.java:399-411): (int) narrowing, null slots 1,
+  // an all-null repeating vector is left alone, isRepeating is not computed
+  if (!is_null) return d->next(vector, n, nullptr);
+  if (is_repeating && n > 0 && is_null[0]) return ORCG_OK;
+  std::vector<char> nn(n);
+  for (uint64_t i = 0; i < n; ++i) nn[i] = is_null[i] ? 0 : 1;
+  const int rc = d->next(vector, n, nn.data());
+  if (rc) return rc;
+  for (uint64_t i = 0; i < n; ++i)
+    if (is_null[i]) vector[i] = 1;
+  return ORCG_OK;
+}
+
 const char* orcg_rle_decoder_last_error(const orcg_rle_decoder* d) {
   return d ? d->last_error.c_str() : "";
 }

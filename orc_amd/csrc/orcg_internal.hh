@@ -101,6 +101,14 @@ int launch_rg_segtab(Ctx* ctx, const int64_t* d_trip, const int64_t* d_prefix, u
                      uint64_t* d_seg);
 int launch_rg_child_rows(Ctx* ctx, const int64_t* d_offsets, const int64_t* d_rows, uint64_t G, int64_t* d_out);
 
+// UNION tags (UnionColumnReader): flags[j] = tags[j] == k; the first tag >=
+// nchildren as (index << 8 | tag), ~0 when none; offsets[j] = scan_k[j] for
+// the rows with tag k.
+int launch_union_flags(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t k, int64_t* d_flags);
+int launch_union_check(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t nchildren, uint64_t* d_first_bad);
+int launch_union_offsets(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t k, const int64_t* d_scan_k,
+                         int64_t* d_offsets);
+
 // Multi-workgroup exclusive scan: d_out[0..n] (n + 1 entries). Scratch 7.
 int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out);
 // Number of non-zero bytes of d_nn[0..n) into *d_total (device). Scratch 5, 6.

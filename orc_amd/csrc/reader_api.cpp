@@ -87,12 +87,12 @@ constexpr int64_t kOrcEpochUtc = 1420070400;
 // (offsets and lengths come from the file and are untrusted)
 bool range_ok(uint64_t off, uint64_t len, uint64_t end) { return off <= end && len <= end - off; }
 
-// Columns this reader decodes: every primitive, list / map / struct, decimals
-// with a precision (Hive 0.11 precision-0 decimals are not), timestamps of
-// UTC writers. Not: UNION.
+// Columns this reader decodes: every primitive, list / map / struct / union,
+// decimals with a precision (Hive 0.11 precision-0 decimals are not),
+// timestamps of UTC writers.
 bool is_supported(const file::TypeInfo& t, const std::string& writer_tz) {
   const uint32_t k = t.kind;
-  if (k == ORCG_TYPE_UNION) return false;
+  if (k == ORCG_TYPE_UNION) return true;
   if (k == ORCG_TYPE_DECIMAL) return t.precision != 0;
   if (k == ORCG_TYPE_TIMESTAMP) return utc_zone(writer_tz);
   if (k == ORCG_TYPE_TIMESTAMP_INSTANT) return true;
@@ -161,6 +161,9 @@ struct Col {
   uint64_t dict_size = 0;  // ColumnEncoding.dictionarySize of this stripe
   bool supported = false;  // decoded by this reader (is_supported for this stripe's writer zone)
   int64_t* secondary = nullptr;  // TIMESTAMP nanoseconds
+  uint8_t* tags = nullptr;       // UNION: child of each row (UnionVectorBatch::tags)
+  int64_t* index = nullptr;      // dictionary strings: entry of each row (EncodedStringVectorBatch::index)
+  int64_t* dict_offsets = nullptr;  // dictionary strings: dict_size + 1 entry offsets (StringDictionary)
   StreamBuf s[5];  // PRESENT, DATA, LENGTH, DICTIONARY_DATA, SECONDARY
 };
 
@@ -228,6 +231,10 @@ struct ColOut {
   const uint8_t* blob = nullptr;
   uint64_t blob_len = 0;
   const int64_t* secondary = nullptr;
+  const uint8_t* tags = nullptr;
+  const int64_t* index = nullptr;
+  const int64_t* dict_offsets = nullptr;
+  uint64_t dict_size = 0;
 };
 
 // One decoded stripe in HBM: its device allocations and column views.
@@ -250,6 +257,8 @@ struct orcg_reader {
   std::string last_error;
   HostStage stages[2];
   bool decimal_as_long = false;  // PostScript version 1.9999 (UNSTABLE-PRE-2.0): Decimal64V2 columns (Reader.cc:1693-1699)
+  bool lazy_dict = false;
+  std::string software_version;  // orcg_reader_software_version's buffer  // RowReaderOptions::setEnableLazyDecoding: dictionary columns keep index + dictionary only
   std::vector<std::unique_ptr<DevSlot>> slots;  // results of the last read, in stripe order
   size_t nslots = 0;
   // decode() state: the host stage and device slot of the stripe being decoded
@@ -577,8 +586,12 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     }
   } else if (is_string_kind(k)) {
     const bool dict = c.encoding == kDictionary || c.encoding == kDictionaryV2;
-    ORCG_ALLOC(int64_t, start, n);
-    ORCG_ALLOC(int64_t, len, n);
+    int64_t* start = nullptr;
+    int64_t* len = nullptr;
+    if (!(dict && lazy_dict)) {
+      ORCG_ALLOC_TO(int64_t, start, n);
+      ORCG_ALLOC_TO(int64_t, len, n);
+    }
     if (dict) {
       // loadStringDictionary (DictionaryLoader.cc:43-97), then
       // StringDictionaryColumnReader::next (ColumnReader.cc:561-594)
@@ -615,10 +628,18 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if (row_nn) {
         ORCG_ALLOC_TO(int64_t, ridx, n);
         if ((rc = scatter(idx, row_nn, n, ridx, 8))) return fail_ctx(rc);
-        if ((rc = hip_check(ctx, hipMemsetAsync(start, 0, n * 8, ctx->stream), "memset"))) return fail_ctx(rc);
-        if ((rc = hip_check(ctx, hipMemsetAsync(len, 0, n * 8, ctx->stream), "memset"))) return fail_ctx(rc);
       }
-      if ((rc = launch_dict_gather(ctx, ridx, 8, row_nn, n, doff, dict_size, start, len))) return fail_ctx(rc);
+      c.index = ridx;
+      c.dict_offsets = doff;
+      if (!lazy_dict) {
+        // StringDictionaryColumnReader::next: bounds-checked gather; nextEncoded
+        // (lazy) hands out the indices and the dictionary unchecked (:596-607)
+        if (row_nn) {
+          if ((rc = hip_check(ctx, hipMemsetAsync(start, 0, n * 8, ctx->stream), "memset"))) return fail_ctx(rc);
+          if ((rc = hip_check(ctx, hipMemsetAsync(len, 0, n * 8, ctx->stream), "memset"))) return fail_ctx(rc);
+        }
+        if ((rc = launch_dict_gather(ctx, ridx, 8, row_nn, n, doff, dict_size, start, len))) return fail_ctx(rc);
+      }
     } else {
       if (!has_len) return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDirectColumn");
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDirectColumn");
@@ -674,6 +695,63 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   } else if (k == ORCG_TYPE_STRUCT) {
     for (uint32_t st : footer.types[id].subtypes)
       if ((rc = decode(st, n, c.nn, nonnull, rg_rows))) return rc;
+  } else if (k == ORCG_TYPE_UNION) {
+    // UnionColumnReader (ColumnReader.cc:1158-1274): byte-RLE tags for the
+    // non-null rows; each row's offset is its rank among the rows of its
+    // tag; child k reads as many rows as carry tag k
+    if (!has_data) return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in Union column");
+    const std::vector<uint32_t> subs = footer.types[id].subtypes;
+    const uint32_t nch = (uint32_t)subs.size();
+    ORCG_ALLOC(uint8_t, dtags, nonnull + 8);
+    if ((rc = byte_stream(c, kSlotData, false, nonnull, dtags))) return rc;
+    ORCG_ALLOC(uint64_t, bad, 1);
+    if ((rc = launch_union_check(ctx, dtags, nonnull, nch, bad))) return fail_ctx(rc);
+    ORCG_ALLOC(int64_t, doffs, nonnull);
+    ORCG_ALLOC(int64_t, flags, nonnull);
+    // dense index of each row group's first row (children's row groups)
+    const int64_t* dense_rows = rg_rows;
+    if (rg_rows && H->ngroups && row_nn) {
+      ORCG_ALLOC(int64_t, cnt, H->ngroups);
+      ORCG_ALLOC(int64_t, pre, H->ngroups + 1);
+      if ((rc = launch_rg_prefix(ctx, row_nn, n, rg_rows, H->ngroups, cnt, pre))) return fail_ctx(rc);
+      dense_rows = pre;
+    }
+    std::vector<int64_t*> scans(nch, nullptr);
+    std::vector<uint64_t> counts(nch, 0);
+    for (uint32_t kk = 0; kk < nch; ++kk) {
+      ORCG_ALLOC_TO(int64_t, scans[kk], nonnull + 1);
+      if ((rc = launch_union_flags(ctx, dtags, nonnull, kk, flags)) ||
+          (rc = launch_exclusive_scan(ctx, flags, nonnull, scans[kk])) ||
+          (rc = launch_union_offsets(ctx, dtags, nonnull, kk, scans[kk], doffs)) ||
+          (rc = hip_check(ctx, hipMemcpyAsync(&counts[kk], scans[kk] + nonnull, 8, hipMemcpyDeviceToHost,
+                                              ctx->stream), "D2H union count")))
+        return fail_ctx(rc);
+    }
+    uint64_t first_bad = ~0ull;
+    if ((rc = hip_check(ctx, hipMemcpyAsync(&first_bad, bad, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
+        (rc = sync_ctx(ctx)))
+      return fail_ctx(rc);
+    if (first_bad != ~0ull)
+      return fail(ORCG_PARSE_ERROR, "Invalid union tag " + std::to_string(first_bad & 0xff) + " for union with " +
+                                        std::to_string(nch) + " children");
+    if (row_nn) {
+      ORCG_ALLOC(uint8_t, rtags, n);
+      ORCG_ALLOC(int64_t, roffs, n);
+      if ((rc = scatter(dtags, row_nn, n, rtags, 1)) || (rc = scatter(doffs, row_nn, n, roffs, 8))) return fail_ctx(rc);
+      c.tags = rtags;
+      c.offsets = roffs;
+    } else {
+      c.tags = dtags;
+      c.offsets = doffs;
+    }
+    for (uint32_t kk = 0; kk < nch; ++kk) {
+      int64_t* child_rows = nullptr;
+      if (dense_rows && H->ngroups) {
+        ORCG_ALLOC_TO(int64_t, child_rows, H->ngroups);
+        if ((rc = launch_rg_child_rows(ctx, scans[kk], dense_rows, H->ngroups, child_rows))) return fail_ctx(rc);
+      }
+      if ((rc = decode(subs[kk], counts[kk], nullptr, counts[kk], child_rows))) return rc;
+    }
   }
   return ORCG_OK;
 }
@@ -691,10 +769,17 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   std::string err;
   std::vector<uint8_t> fb;
   // stripe = [offset, + index, + data, + footer), every sum checked
-  uint64_t foff = 0;
+  // (RowReaderImpl::startNextStripe, Reader.cc:1257-1268)
+  uint64_t foff = 0, total = 0;
   if (__builtin_add_overflow(si.offset, si.index_length, &foff) ||
-      __builtin_add_overflow(foff, si.data_length, &foff) || !range_ok(foff, si.footer_length, file_len))
-    return hs.fail(ORCG_PARSE_ERROR, "stripe footer past the end of the file");
+      __builtin_add_overflow(foff, si.data_length, &foff) ||
+      __builtin_add_overflow(foff, si.footer_length, &total) || total >= file_len)
+    return hs.fail(ORCG_PARSE_ERROR, "Malformed StripeInformation at stripe index " + std::to_string(s) +
+                                         ": fileLength=" + std::to_string(file_len) + ", StripeInfo=(offset=" +
+                                         std::to_string(si.offset) + ", indexLength=" +
+                                         std::to_string(si.index_length) + ", dataLength=" +
+                                         std::to_string(si.data_length) + ", footerLength=" +
+                                         std::to_string(si.footer_length) + ")");
   if (!read_range(file, foff, si.footer_length, ps.compression, ps.block_size, fb, err))
     return hs.fail(ORCG_PARSE_ERROR, err);
   StripeFooter sf;
@@ -797,7 +882,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
       if (c.s[kSlotPresent].present) order.push_back({kSlotPresent, kBool});
       const bool dict = c.encoding == kDictionary || c.encoding == kDictionaryV2;
       if (k == ORCG_TYPE_BOOLEAN) order.push_back({kSlotData, kBool});
-      else if (k == ORCG_TYPE_BYTE) order.push_back({kSlotData, kByteRle});
+      else if (k == ORCG_TYPE_BYTE || k == ORCG_TYPE_UNION) order.push_back({kSlotData, kByteRle});
       else if (is_int_kind(k)) order.push_back({kSlotData, kInt});
       else if (k == ORCG_TYPE_FLOAT || k == ORCG_TYPE_DOUBLE) order.push_back({kSlotData, kRaw});
       else if (is_string_kind(k)) {
@@ -906,7 +991,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
       int kind;
       if (sl == kSlotPresent) kind = 0;
       else if (sl == kSlotData) {
-        if (c.kind == ORCG_TYPE_BOOLEAN || c.kind == ORCG_TYPE_BYTE) kind = 0;
+        if (c.kind == ORCG_TYPE_BOOLEAN || c.kind == ORCG_TYPE_BYTE || c.kind == ORCG_TYPE_UNION) kind = 0;
         else if (is_int_kind(c.kind) || c.kind == ORCG_TYPE_TIMESTAMP || c.kind == ORCG_TYPE_TIMESTAMP_INSTANT ||
                  (is_string_kind(c.kind) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)))
           kind = v1 ? 1 : 2;
@@ -1024,6 +1109,10 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
     o.blob = c.blob;
     o.blob_len = c.blob_len;
     o.secondary = c.secondary;
+    o.tags = c.tags;
+    o.index = c.index;
+    o.dict_offsets = c.dict_offsets;
+    o.dict_size = c.dict_offsets ? c.dict_size : 0;
   }
   H = nullptr;
   D = nullptr;
@@ -1072,6 +1161,81 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   }
   return ORCG_OK;
 }
+
+// ---- RowReader: batches of at most `capacity` rows over the stripes of a
+// byte range (c++/src/Reader.cc RowReaderImpl: ctor :307-363, next
+// :1392-1442, seekToRow :428-499, getRowNumber :424-426, markEndOfFile
+// :1128-1139). The GPU decodes a whole stripe into HBM once; each batch is a
+// row range of it (per column: an element range, through list / map offsets
+// and union tags), which the host adapters copy out.
+struct orcg_row_reader {
+  orcg_reader* r = nullptr;
+  uint64_t nstripes = 0, first = 0, last = 0;  // stripes [first, last) are in range
+  uint64_t current = 0, row_in_stripe = 0, rows_in_stripe = 0;
+  uint64_t previous_row = 0;
+  std::vector<uint64_t> first_row;  // firstRowOfStripe_
+  uint64_t loaded = ~0ull;          // stripe decoded in the reader's slot 0
+  uint64_t batch_stripe = ~0ull, batch_row0 = 0, batch_rows = 0;
+  std::vector<uint64_t> begin, count;  // per type id: element range of the current batch
+  std::vector<uint8_t> in_batch;
+
+  void mark_end_of_file() {
+    current = last;
+    row_in_stripe = 0;
+    rows_in_stripe = 0;
+    previous_row = last == 0 ? 0 : first_row[last - 1] + r->footer.stripes[last - 1].num_rows;
+  }
+  int load(uint64_t s) {
+    if (loaded == s && r->nslots >= 1 && r->slots[0]->stripe == s) return ORCG_OK;
+    loaded = ~0ull;
+    const int rc = r->read_stripes(s, 1);
+    if (rc) return rc;
+    loaded = s;
+    return ORCG_OK;
+  }
+  int d2h(void* dst, const void* src, uint64_t bytes) {
+    int rc = hip_check(r->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, r->ctx->stream), "D2H");
+    if (!rc) rc = sync_ctx(r->ctx);
+    return rc ? r->fail_ctx(rc) : ORCG_OK;
+  }
+  // element range [b, b + c) of column `id` and, recursively, its children
+  int ranges(uint32_t id, uint64_t b, uint64_t c) {
+    const ColOut& o = r->slots[0]->out[id];
+    if (!o.decoded) return ORCG_OK;
+    begin[id] = b;
+    count[id] = c;
+    in_batch[id] = 1;
+    const auto& t = r->footer.types[id];
+    int rc;
+    if (t.kind == ORCG_TYPE_STRUCT) {
+      for (uint32_t st : t.subtypes)
+        if ((rc = ranges(st, b, c))) return rc;
+    } else if (t.kind == ORCG_TYPE_LIST || t.kind == ORCG_TYPE_MAP) {
+      int64_t ends[2] = {0, 0};
+      if ((rc = d2h(&ends[0], o.offsets + b, 8)) || (rc = d2h(&ends[1], o.offsets + b + c, 8))) return rc;
+      for (uint32_t st : t.subtypes)
+        if ((rc = ranges(st, (uint64_t)ends[0], (uint64_t)(ends[1] - ends[0])))) return rc;
+    } else if (t.kind == ORCG_TYPE_UNION) {
+      // child k's rows are the ranks of this batch's non-null tag-k rows
+      std::vector<uint8_t> tags(c), nn(c, 1);
+      std::vector<int64_t> offs(c);
+      if (c && ((rc = d2h(tags.data(), o.tags + b, c)) || (rc = d2h(offs.data(), o.offsets + b, 8 * c)) ||
+                (o.has_nulls && (rc = d2h(nn.data(), o.nn + b, c)))))
+        return rc;
+      for (uint32_t k = 0; k < t.subtypes.size(); ++k) {
+        uint64_t cb = ~0ull, cc = 0;
+        for (uint64_t i = 0; i < c; ++i)
+          if (nn[i] && tags[i] == k) {
+            if (cb == ~0ull) cb = (uint64_t)offs[i];
+            ++cc;
+          }
+        if (cb == ~0ull) cb = 0;  // no row of this batch carries tag k: an empty range
+        if ((rc = ranges(t.subtypes[k], cb, cc))) return rc;
+      }
+    }
+    return ORCG_OK;
+  }
+};
 
 static thread_local std::string t_open_error;
 
@@ -1138,6 +1302,30 @@ uint32_t orcg_reader_row_index_stride(const orcg_reader* r) { return r ? r->foot
 uint32_t orcg_reader_compression(const orcg_reader* r) { return r ? r->ps.compression : 0; }
 uint64_t orcg_reader_compression_block_size(const orcg_reader* r) { return r ? r->ps.block_size : 0; }
 uint32_t orcg_reader_writer_version(const orcg_reader* r) { return r ? r->ps.writer_version : 0; }
+uint64_t orcg_reader_content_length(const orcg_reader* r) { return r ? r->footer.content_length : 0; }
+const char* orcg_reader_software_version(const orcg_reader* r) {
+  if (!r) return "";
+  static const char* kNames[] = {"ORC Java", "ORC C++", "Presto", "Scritchley Go", "Trino", "CUDF"};
+  auto* rr = const_cast<orcg_reader*>(r);
+  const uint32_t id = r->footer.writer;
+  rr->software_version = id < 6 ? kNames[id] : "Unknown(" + std::to_string(id) + ")";
+  if (r->footer.has_software_version) rr->software_version += " " + r->footer.software_version;
+  return rr->software_version.c_str();
+}
+uint32_t orcg_reader_num_metadata(const orcg_reader* r) { return r ? (uint32_t)r->footer.metadata.size() : 0; }
+const char* orcg_reader_metadata_key(const orcg_reader* r, uint32_t i) {
+  return r && i < r->footer.metadata.size() ? r->footer.metadata[i].first.c_str() : nullptr;
+}
+const uint8_t* orcg_reader_metadata_value(const orcg_reader* r, uint32_t i, uint64_t* len) {
+  if (!r || i >= r->footer.metadata.size()) return nullptr;
+  if (len) *len = r->footer.metadata[i].second.size();
+  return (const uint8_t*)r->footer.metadata[i].second.data();
+}
+int orcg_reader_set_lazy_dictionary(orcg_reader* r, int on) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  r->lazy_dict = on != 0;
+  return ORCG_OK;
+}
 int orcg_reader_format_version(const orcg_reader* r, uint32_t* major, uint32_t* minor) {
   if (!r || !major || !minor) return ORCG_INVALID_ARGUMENT;
   // the reference reports 0.11 when the version is absent (FileVersion::v_0_11)
@@ -1205,6 +1393,10 @@ int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes) 
   return ORCG_OK;
 }
 
+int orcg_reader_is_selected(const orcg_reader* r, uint32_t type_id) {
+  return r && type_id < r->selected.size() && r->selected[type_id] ? 1 : 0;
+}
+
 int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe) {
   if (!r) return ORCG_INVALID_ARGUMENT;
   return r->read_stripes(stripe, 1);
@@ -1233,6 +1425,10 @@ int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t id, orc
   out->blob = c.blob;
   out->blob_len = c.blob_len;
   out->secondary = c.secondary;
+  out->tags = c.tags;
+  out->index = c.index;
+  out->dict_offsets = c.dict_offsets;
+  out->dict_size = c.dict_size;
   return ORCG_OK;
 }
 
@@ -1246,6 +1442,126 @@ int orcg_reader_copy_to_host(orcg_reader* r, void* dst, const void* src, uint64_
   int rc = hip_check(r->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, r->ctx->stream), "D2H");
   if (!rc) rc = sync_ctx(r->ctx);
   return rc;
+}
+
+int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orcg_row_reader** out) {
+  if (!r || !out) return ORCG_INVALID_ARGUMENT;
+  *out = nullptr;
+  if (!r->ctx) return r->fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
+  const uint64_t off = o ? o->offset : 0;
+  const uint64_t len = o ? o->length : ~0ull;
+  if (o) {
+    int rc = orcg_reader_select(r, o->include, o->include ? o->include_len : 0);
+    if (rc) return rc;
+    r->lazy_dict = o->lazy_dictionary != 0;
+  }
+  std::unique_ptr<orcg_row_reader> rr(new orcg_row_reader());
+  rr->r = r;
+  const uint64_t ns = r->footer.stripes.size();
+  rr->nstripes = ns;
+  rr->current = ns;
+  rr->last = 0;
+  rr->first_row.resize(ns);
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < ns; ++i) {
+    rr->first_row[i] = total;
+    const StripeInfo& si = r->footer.stripes[i];
+    total += si.num_rows;
+    // isStripeInRange: offset in [off, off + len), without wrapping
+    if (si.offset >= off && si.offset - off < len) {
+      if (i < rr->current) rr->current = i;
+      if (i >= rr->last) rr->last = i + 1;
+    }
+  }
+  rr->first = rr->current;
+  if (rr->current == 0) rr->previous_row = ~0ull;
+  else if (rr->current == ns) rr->previous_row = r->footer.num_rows;
+  else rr->previous_row = rr->first_row[rr->first] - 1;
+  const size_t nt = r->footer.types.size();
+  rr->begin.assign(nt, 0);
+  rr->count.assign(nt, 0);
+  rr->in_batch.assign(nt, 0);
+  *out = rr.release();
+  return ORCG_OK;
+}
+
+void orcg_row_reader_destroy(orcg_row_reader* rr) { delete rr; }
+
+int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows) {
+  if (!rr || !rows) return ORCG_INVALID_ARGUMENT;
+  *rows = 0;
+  std::fill(rr->in_batch.begin(), rr->in_batch.end(), 0);
+  rr->batch_rows = 0;
+  if (rr->current >= rr->last) {
+    rr->mark_end_of_file();
+    return ORCG_OK;
+  }
+  int rc;
+  if (rr->row_in_stripe == 0 || rr->loaded != rr->current) {
+    // startNextStripe
+    if ((rc = rr->load(rr->current))) return rc;
+    rr->rows_in_stripe = rr->r->footer.stripes[rr->current].num_rows;
+  }
+  const uint64_t n = std::min(capacity, rr->rows_in_stripe - rr->row_in_stripe);
+  if (n == 0) {
+    rr->mark_end_of_file();
+    return ORCG_OK;
+  }
+  rr->batch_stripe = rr->current;
+  rr->batch_row0 = rr->row_in_stripe;
+  rr->batch_rows = n;
+  if ((rc = rr->ranges(0, rr->row_in_stripe, n))) return rc;
+  rr->previous_row = rr->first_row[rr->current] + rr->row_in_stripe;
+  rr->row_in_stripe += n;
+  if (rr->row_in_stripe >= rr->rows_in_stripe) {
+    rr->current += 1;
+    rr->row_in_stripe = 0;
+  }
+  *rows = n;
+  return ORCG_OK;
+}
+
+uint64_t orcg_row_reader_row_number(const orcg_row_reader* rr) { return rr ? rr->previous_row : 0; }
+
+int orcg_row_reader_seek_to_row(orcg_row_reader* rr, uint64_t row) {
+  if (!rr) return ORCG_INVALID_ARGUMENT;
+  if (rr->last == 0) return ORCG_OK;  // empty file / range
+  const uint64_t ns = rr->nstripes;
+  const uint64_t nrows = rr->r->footer.num_rows;
+  if ((rr->last == ns && row >= nrows) || (rr->last < ns && row >= rr->first_row[rr->last])) {
+    rr->current = ns;
+    rr->previous_row = nrows;
+    return ORCG_OK;
+  }
+  uint64_t s = 0;
+  while (s + 1 < rr->last && rr->first_row[s + 1] <= row) ++s;
+  if (s < rr->first) {
+    rr->current = ns;
+    rr->previous_row = nrows;
+    return ORCG_OK;
+  }
+  rr->previous_row = row;
+  rr->current = s;
+  rr->row_in_stripe = row - rr->first_row[s];
+  int rc = rr->load(s);
+  if (rc) return rc;
+  rr->rows_in_stripe = rr->r->footer.stripes[s].num_rows;
+  return ORCG_OK;
+}
+
+int orcg_row_reader_column(const orcg_row_reader* rr, uint32_t id, orcg_column_view* view, uint64_t* begin,
+                           uint64_t* count) {
+  if (!rr || !view || !begin || !count || id >= rr->in_batch.size()) return ORCG_INVALID_ARGUMENT;
+  memset(view, 0, sizeof(*view));
+  view->type_id = id;
+  view->kind = rr->r->footer.types[id].kind;
+  *begin = *count = 0;
+  if (!rr->in_batch[id]) return ORCG_OK;  // no batch, or the column is not decoded
+  const int rc = orcg_reader_stripe_column(rr->r, 0, id, view);
+  if (rc) return rc;
+  *begin = rr->begin[id];
+  *count = rr->count[id];
+  return ORCG_OK;
 }
 
 int orcg_reader_last_timings(const orcg_reader* r, double* out5) {

@@ -2,13 +2,17 @@
 
 Mirrors the reference's reader surface for the decode path
 (c++/include/orc/Reader.hh: createReader, getNumberOfRows,
-getNumberOfStripes, getType, RowReader::next) with one stripe per read:
-the host parses the tail and stripe footers and decompresses, the GPU decodes
-every selected column into device batches (LongVectorBatch / DoubleVectorBatch
-/ StringVectorBatch / ListVectorBatch / MapVectorBatch / StructVectorBatch
-layouts, c++/include/orc/Vector.hh:46-330). `Batch.to_pylist()` renders rows
-the way the reference's ColumnPrinter / pyarrow's to_pylist do, for parity
-tests.
+getNumberOfStripes, getType, getContentLength, getSoftwareVersion,
+getMetadataKeys / getMetadataValue; RowReader createRowBatch(capacity),
+next(batch), getRowNumber, seekToRow; RowReaderOptions include / range /
+setEnableLazyDecoding): the host parses the tail and stripe footers and
+decompresses, the GPU decodes every selected column of a stripe into device
+batches (LongVectorBatch / DoubleVectorBatch / StringVectorBatch /
+EncodedStringVectorBatch / ListVectorBatch / MapVectorBatch /
+StructVectorBatch / UnionVectorBatch layouts, c++/include/orc/Vector.hh:
+46-352), and RowReader batches are row ranges of that stripe copied to host.
+`Batch.to_pylist()` renders rows the way the reference's ColumnPrinter /
+pyarrow's to_pylist do, for parity tests.
 """
 import ctypes
 import datetime
@@ -27,8 +31,26 @@ KIND_NAMES = ["boolean", "tinyint", "smallint", "int", "bigint", "float", "doubl
               "timestamp with local time zone"]
 COMPRESSION_NAMES = ["NONE", "ZLIB", "SNAPPY", "LZO", "LZ4", "ZSTD"]
 SUPPORTED = {BOOLEAN, BYTE, SHORT, INT, LONG, FLOAT, DOUBLE, STRING, BINARY, LIST, MAP, STRUCT, DATE, VARCHAR,
-             CHAR}
+             CHAR, UNION}
+STRING_KINDS = (STRING, VARCHAR, CHAR, BINARY)
 _EPOCH = datetime.date(1970, 1, 1)
+
+
+class UnionValue(tuple):
+    """One UNION row: (tag, value) — UnionVectorBatch tags / offsets resolved."""
+
+    __slots__ = ()
+
+    def __new__(cls, tag, value):
+        return tuple.__new__(cls, (tag, value))
+
+    @property
+    def tag(self):
+        return self[0]
+
+    @property
+    def value(self):
+        return self[1]
 
 
 class Type:
@@ -50,16 +72,20 @@ class Type:
 class ColumnBatch:
     """Host copy of one column's device batch."""
 
-    def __init__(self, kind, n, not_null, data, length, offsets, blob, encoding, secondary=None):
+    def __init__(self, kind, n, not_null, data, length, offsets, blob, encoding, secondary=None, tags=None,
+                 index=None, dict_offsets=None):
         self.kind = kind
         self.secondary = secondary  # np.int64[n] TIMESTAMP nanoseconds
         self.num_elements = n
         self.not_null = not_null  # np.uint8[n] or None
         self.data = data          # np.int64 / np.float64 [n] (string starts for string kinds)
         self.length = length      # np.int64[n] for string kinds
-        self.offsets = offsets    # np.int64[n + 1] for list / map
+        self.offsets = offsets    # np.int64[n + 1] for list / map; np.int64[n] child offsets for union
         self.blob = blob          # bytes for string kinds
         self.encoding = encoding
+        self.tags = tags          # np.uint8[n] UNION child per row
+        self.index = index        # np.int64[n] dictionary entry per row (EncodedStringVectorBatch::index)
+        self.dict_offsets = dict_offsets  # np.int64[dict_size + 1] into blob (StringDictionary)
 
 
 class Batch:
@@ -100,8 +126,12 @@ class Batch:
         if k in (TIMESTAMP, TIMESTAMP_INSTANT):
             # TimestampVectorBatch seconds + nanoseconds, as numpy datetime64[ns]
             return np.datetime64(int(c.data[i]) * 1_000_000_000 + int(c.secondary[i]), "ns")
-        if k in (STRING, VARCHAR, CHAR, BINARY):
-            s, ln = int(c.data[i]), int(c.length[i])
+        if k in STRING_KINDS:
+            if c.data is None:  # lazy dictionary: index + dictionary
+                e = int(c.index[i])
+                s, ln = int(c.dict_offsets[e]), int(c.dict_offsets[e + 1] - c.dict_offsets[e])
+            else:
+                s, ln = int(c.data[i]), int(c.length[i])
             raw = c.blob[s:s + ln]
             return raw if k == BINARY else raw.decode("utf-8", errors="replace")
         if k == LIST:
@@ -112,11 +142,17 @@ class Batch:
             return [(self.value(t.subtypes[0], j), self.value(t.subtypes[1], j)) for j in range(a, b)]
         if k == STRUCT:
             return {name: self.value(st, i) for name, st in zip(t.field_names, t.subtypes)}
+        if k == UNION:
+            tag = int(c.tags[i])
+            return UnionValue(tag, self.value(t.subtypes[tag], int(c.offsets[i])))
         raise KeyError("type %s not decoded" % KIND_NAMES[k])
 
     def to_pylist(self, fields=None):
-        """Rows of the root struct as dicts (pyarrow Table.to_pylist shape)."""
+        """Rows of the root struct as dicts (pyarrow Table.to_pylist shape);
+        a non-struct root gives its values."""
         root = self.reader.types[0]
+        if root.kind != STRUCT:
+            return [self.value(0, i) for i in range(self.num_rows)]
         names = [n for n in root.field_names if fields is None or n in fields]
         ids = {n: st for n, st in zip(root.field_names, root.subtypes)}
         return [{n: self.value(ids[n], i) for n in names} for i in range(self.num_rows)]
@@ -264,6 +300,56 @@ class Reader:
         check(self._L.orcg_reader_stripe_column(self._h, k, tid, ctypes.byref(v)), self._err)
         return v
 
+    def _column(self, v, t, begin=0, count=None):
+        """Host copy of elements [begin, begin + count) of a device column
+        view (the whole column by default): offsets rebased to 0 (the
+        reference's batch layout), string starts relative to the copied blob
+        (the dictionary, or the span of direct strings the range covers)."""
+        n = v.num_elements if count is None else count
+        k = t.kind
+
+        def host(ptr, itemsize, dtype, cnt, first=begin):
+            if not ptr or cnt <= 0:
+                return np.zeros(max(cnt, 0), dtype=dtype)
+            return self._host(ptr + first * itemsize, cnt * itemsize, dtype)
+
+        nn = host(v.not_null, 1, np.uint8, n) if v.has_nulls else None
+        data = length = offsets = tags = index = dict_offsets = secondary = None
+        blob = b""
+        if k in (FLOAT, DOUBLE):
+            data = host(v.data, 8, np.float64, n)
+        elif k in (BOOLEAN, BYTE, SHORT, INT, LONG, DATE):
+            data = host(v.data, 8, np.int64, n)
+        elif k in STRING_KINDS:
+            if v.index:
+                index = host(v.index, 8, np.int64, n)
+                dict_offsets = self._host(v.dict_offsets, 8 * (v.dict_size + 1), np.int64)
+            if v.data:
+                data = host(v.data, 8, np.int64, n)
+                length = host(v.length, 8, np.int64, n)
+            if v.index and v.dict_offsets:
+                blob = self._host(v.blob, v.blob_len, np.uint8).tobytes()  # the dictionary
+            elif data is not None and n:
+                live = length > 0
+                lo = int(data[live].min()) if live.any() else 0
+                hi = int((data + length)[live].max()) if live.any() else 0
+                blob = host(v.blob, 1, np.uint8, hi - lo, first=lo).tobytes()
+                data = np.where(live, data - lo, 0)
+        elif k in (LIST, MAP):
+            offsets = host(v.offsets, 8, np.int64, n + 1)
+            offsets = offsets - offsets[0] if offsets.size else offsets
+        elif k == UNION:
+            tags = host(v.tags, 1, np.uint8, n)
+            offsets = host(v.offsets, 8, np.int64, n)
+        if k == DECIMAL:
+            w = 16 if t.precision > 18 else 8
+            data = host(v.data, w, np.int64, n).reshape(-1) if w == 8 else \
+                self._host(v.data + begin * 16, 16 * n, np.int64) if n else np.zeros(0, np.int64)
+        elif k in (TIMESTAMP, TIMESTAMP_INSTANT):
+            data = host(v.data, 8, np.int64, n)
+            secondary = host(v.secondary, 8, np.int64, n)
+        return ColumnBatch(k, n, nn, data, length, offsets, blob, v.encoding, secondary, tags, index, dict_offsets)
+
     def read_stripe(self, i):
         """Decode stripe i on the GPU and copy the selected columns to host."""
         self.read_stripe_device(i)
@@ -272,29 +358,39 @@ class Reader:
             v = _lib.ColumnView()
             if self._L.orcg_reader_column(self._h, t.id, ctypes.byref(v)) != 0 or not v.decoded:
                 continue
-            n = v.num_elements
-            nn = self._host(v.not_null, n, np.uint8) if v.has_nulls else None
-            data = length = offsets = None
-            blob = b""
-            k = t.kind
-            if k in (FLOAT, DOUBLE):
-                data = self._host(v.data, 8 * n, np.float64)
-            elif k in (BOOLEAN, BYTE, SHORT, INT, LONG, DATE):
-                data = self._host(v.data, 8 * n, np.int64)
-            elif k in (STRING, VARCHAR, CHAR, BINARY):
-                data = self._host(v.data, 8 * n, np.int64)
-                length = self._host(v.length, 8 * n, np.int64)
-                blob = self._host(v.blob, v.blob_len, np.uint8).tobytes()
-            elif k in (LIST, MAP):
-                offsets = self._host(v.offsets, 8 * (n + 1), np.int64)
-            secondary = None
-            if k == DECIMAL:
-                data = self._host(v.data, (16 if t.precision > 18 else 8) * n, np.int64)
-            elif k in (TIMESTAMP, TIMESTAMP_INSTANT):
-                data = self._host(v.data, 8 * n, np.int64)
-                secondary = self._host(v.secondary, 8 * n, np.int64)
-            cols[t.id] = ColumnBatch(k, n, nn, data, length, offsets, blob, v.encoding, secondary)
+            cols[t.id] = self._column(v, t)
         return Batch(self, cols)
+
+    @property
+    def content_length(self):
+        """Reader::getContentLength (Footer.contentLength)."""
+        return self._L.orcg_reader_content_length(self._h)
+
+    @property
+    def software_version(self):
+        """Reader::getSoftwareVersion: writer id name [+ softwareVersion]."""
+        return self._L.orcg_reader_software_version(self._h).decode()
+
+    @property
+    def metadata(self):
+        """User metadata (Reader::getMetadataKeys / getMetadataValue) as bytes values."""
+        out = {}
+        for i in range(self._L.orcg_reader_num_metadata(self._h)):
+            key = self._L.orcg_reader_metadata_key(self._h, i).decode()
+            ln = ctypes.c_uint64()
+            p = self._L.orcg_reader_metadata_value(self._h, i, ctypes.byref(ln))
+            out[key] = ctypes.string_at(p, ln.value) if p and ln.value else b""
+        return out
+
+    def set_lazy_dictionary(self, on=True):
+        """RowReaderOptions::setEnableLazyDecoding for stripe reads."""
+        check(self._L.orcg_reader_set_lazy_dictionary(self._h, int(bool(on))), self._err)
+
+    def create_row_reader(self, include=None, offset=0, length=None, lazy_dictionary=False):
+        """Reader::createRowReader(RowReaderOptions): `include` type ids (or
+        top-level field names), range(offset, length) in file bytes,
+        setEnableLazyDecoding."""
+        return RowReader(self, include=include, offset=offset, length=length, lazy_dictionary=lazy_dictionary)
 
     def last_timings(self):
         t = (ctypes.c_double * 5)()
@@ -316,6 +412,98 @@ class Reader:
         return rows
 
 
+class RowBatch(Batch):
+    """A batch of at most `capacity` rows (RowReader::createRowBatch)."""
+
+    def __init__(self, reader, capacity):
+        super().__init__(reader, {})
+        self.capacity = capacity
+        self.num_elements = 0
+
+    @property
+    def num_rows(self):
+        return self.num_elements
+
+
+class RowReader:
+    """orc::RowReader (c++/include/orc/Reader.hh:640-790) over the GPU stripe
+    decode (include/orcg_reader.h orcg_row_reader_*): next(batch) fills at
+    most batch.capacity rows and never crosses a stripe
+    (RowReaderImpl::next, c++/src/Reader.cc:1392-1442); get_row_number /
+    seek_to_row follow RowReaderImpl (:424-499); range(offset, length)
+    selects the stripes whose offset falls in the byte range (:337-345)."""
+
+    def __init__(self, reader, include=None, offset=0, length=None, lazy_dictionary=False):
+        if reader._ctx is None:
+            raise _lib.InvalidArgument("reader was opened without a device context")
+        self.reader = reader
+        self._L = reader._L
+        opts = _lib.RowReaderOptions()
+        opts.offset = offset
+        opts.length = (1 << 64) - 1 if length is None else length
+        self._inc = None
+        if include is not None:
+            root = reader.types[0]
+            ids = [root.subtypes[root.field_names.index(x)] if isinstance(x, str) else int(x) for x in include]
+            self._inc = np.zeros(len(reader.types), dtype=np.uint8)
+            self._inc[ids] = 1
+            opts.include = self._inc.ctypes.data_as(ctypes.c_void_p)
+            opts.include_len = self._inc.size
+        opts.lazy_dictionary = int(bool(lazy_dictionary))
+        h = ctypes.c_void_p()
+        check(self._L.orcg_row_reader_create(reader._h, ctypes.byref(opts), ctypes.byref(h)), reader._err)
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.orcg_row_reader_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def create_row_batch(self, capacity):
+        return RowBatch(self.reader, int(capacity))
+
+    def next(self, batch):
+        """RowReader::next: True with batch.num_elements rows, False at the end."""
+        rows = ctypes.c_uint64()
+        check(self._L.orcg_row_reader_next(self._h, batch.capacity, ctypes.byref(rows)), self.reader._err)
+        batch.num_elements = rows.value
+        batch.columns = {}
+        if rows.value == 0:
+            return False
+        begins = {}
+        for t in self.reader.types:
+            v = _lib.ColumnView()
+            b, c = ctypes.c_uint64(), ctypes.c_uint64()
+            check(self._L.orcg_row_reader_column(self._h, t.id, ctypes.byref(v), ctypes.byref(b), ctypes.byref(c)),
+                  self.reader._err)
+            if v.decoded:
+                batch.columns[t.id] = self.reader._column(v, t, b.value, c.value)
+                begins[t.id] = b.value
+        # union offsets index the stripe's child rows: make them batch-relative
+        for tid, col in batch.columns.items():
+            t = self.reader.types[tid]
+            if t.kind == UNION and col.num_elements:
+                offs = col.offsets.copy()
+                for k, st in enumerate(t.subtypes):
+                    m = col.tags == k
+                    offs[m] -= begins.get(st, 0)
+                if col.not_null is not None:
+                    offs[col.not_null == 0] = 0
+                col.offsets = offs
+        return True
+
+    def get_row_number(self):
+        """RowReader::getRowNumber: first row of the last batch."""
+        return self._L.orcg_row_reader_row_number(self._h)
+
+    def seek_to_row(self, row):
+        """RowReader::seekToRow: the next batch starts at `row`."""
+        check(self._L.orcg_row_reader_seek_to_row(self._h, int(row)), self.reader._err)
+
+
 def open_reader(source, ctx=None, device=True):
     """createReader: `device=False` opens for metadata only (no GPU)."""
     if device and ctx is None:
@@ -323,4 +511,4 @@ def open_reader(source, ctx=None, device=True):
     return Reader(source, ctx)
 
 
-__all__ = ["Reader", "Batch", "ColumnBatch", "Type", "open_reader", "Context"]
+__all__ = ["Reader", "RowReader", "RowBatch", "Batch", "ColumnBatch", "Type", "UnionValue", "open_reader", "Context"]

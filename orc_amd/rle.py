@@ -118,15 +118,29 @@ class RleDecoderV2:
         p = np.asarray(positions, dtype=np.uint64)
         check(self._L.orcg_rle_decoder_seek(self._h, _ptr(p), p.size), self._err)
 
-    def next_vector_java(self, n, is_null=None, is_repeating=False):
-        """Java LongColumnVector semantics: null slots get 1; returns
-        (vector, isRepeating)."""
-        out = np.zeros(n, dtype=np.int64)
+    def next_vector_java(self, n, is_null=None, is_repeating=False, out=None):
+        """IntegerReader.nextVector(ColumnVector, long[], int)
+        (RunLengthIntegerReaderV2.java:371-396): `is_null` None = noNulls;
+        null slots get 1; returns (vector, isRepeating). `out` is the
+        caller's long[] (left untouched by the all-null repeating early-out)."""
+        if out is None:
+            out = np.zeros(n, dtype=np.int64)
         isn = None if is_null is None else np.ascontiguousarray(is_null, dtype=np.uint8)
         rep = ctypes.c_int(1 if is_repeating else 0)
         check(self._L.orcg_rle_decoder_next_vector_java(self._h, _ptr(out), _ptr(isn), n,
                                                          ctypes.byref(rep)), self._err)
         return out, bool(rep.value)
+
+    def next_vector_java_int(self, n, is_null=None, is_repeating=False, out=None):
+        """IntegerReader.nextVector(ColumnVector, int[], int)
+        (RunLengthIntegerReaderV2.java:399-411): (int) narrowing, null slots
+        1; isRepeating is read, not computed."""
+        if out is None:
+            out = np.zeros(n, dtype=np.int32)
+        isn = None if is_null is None else np.ascontiguousarray(is_null, dtype=np.uint8)
+        check(self._L.orcg_rle_decoder_next_vector_java_int(self._h, _ptr(out), _ptr(isn), n,
+                                                             1 if is_repeating else 0), self._err)
+        return out
 
     def close(self):
         if getattr(self, "_h", None):

@@ -30,111 +30,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-DEMO12 = os.path.join(ROOT, "tests", "golden", "files", "demo-12-zlib.orc")
-
-
-def make_c3(path, rows, stripe_mb):
-    import pyarrow as pa
-    import pyarrow.compute as pc
-    import pyarrow.orc as po
-
-    base = po.ORCFile(DEMO12).read()
-    n0 = base.num_rows
-    tiles = max(1, rows // n0)
-    parts = []
-    for t in range(tiles):
-        cols = []
-        for name in base.column_names:
-            c = base.column(name)
-            if name == "_col0":
-                c = pc.add(c, pa.scalar(t * n0, pa.int32()))
-            cols.append(c)
-        parts.append(pa.table(cols, names=base.column_names))
-    table = pa.concat_tables(parts)
-    po.write_table(table, path, compression="zlib", stripe_size=stripe_mb << 20,
-                   dictionary_key_size_threshold=1.0, row_index_stride=10000)
-
-
-def _decimal(pa, cents, precision, scale):
-    """decimal128(precision, scale) array of the int64 unscaled values."""
-    v = np.ascontiguousarray(cents, dtype=np.int64)
-    buf = np.empty((v.size, 2), dtype=np.int64)
-    buf[:, 0] = v
-    buf[:, 1] = v >> 63
-    return pa.Array.from_buffers(pa.decimal128(precision, scale), v.size, [None, pa.py_buffer(buf.tobytes())])
-
-
-def _dict_strings(pa, rng, words, n):
-    idx = pa.array(rng.integers(0, len(words), size=n).astype(np.int32))
-    return pa.DictionaryArray.from_arrays(idx, pa.array(words)).cast(pa.string())
-
-
-def make_c4(path, rows, stripe_mb):
-    import pyarrow as pa
-    import pyarrow.compute as pc
-    import pyarrow.orc as po
-
-    rng = np.random.default_rng(4)
-    reps = rng.integers(1, 8, size=rows // 2 + 8)
-    reps = reps[: np.searchsorted(np.cumsum(reps), rows) + 1]
-    okey = np.repeat(np.arange(1, reps.size + 1, dtype=np.int64) * 4, reps)[:rows]
-    line = (np.arange(okey.size) - np.repeat(np.cumsum(reps) - reps, reps)[:rows] + 1).astype(np.int32)
-    qty = rng.integers(1, 51, size=rows)
-    price = qty * rng.integers(90_000, 210_000, size=rows) // 100
-    ship = rng.integers(8036, 10561, size=rows).astype(np.int32)  # 1992-01-02 .. 1998-12-01
-    pool = pa.array(["".join(chr(97 + c) for c in rng.integers(0, 26, size=int(rng.integers(5, 22))))
-                     for _ in range(4096)])
-    c1 = pc.take(pool, pa.array(rng.integers(0, 4096, size=rows)))
-    c2 = pc.take(pool, pa.array(rng.integers(0, 4096, size=rows)))
-    table = pa.table({
-        "l_orderkey": pa.array(okey),
-        "l_partkey": pa.array(rng.integers(1, 20_000_001, size=rows)),
-        "l_suppkey": pa.array(rng.integers(1, 1_000_001, size=rows)),
-        "l_linenumber": pa.array(line),
-        "l_quantity": _decimal(pa, qty * 100, 15, 2),
-        "l_extendedprice": _decimal(pa, price, 15, 2),
-        "l_discount": _decimal(pa, rng.integers(0, 11, size=rows), 15, 2),
-        "l_tax": _decimal(pa, rng.integers(0, 9, size=rows), 15, 2),
-        "l_returnflag": _dict_strings(pa, rng, ["A", "N", "R"], rows),
-        "l_linestatus": _dict_strings(pa, rng, ["O", "F"], rows),
-        "l_shipdate": pa.array(ship, type=pa.date32()),
-        "l_commitdate": pa.array(ship + rng.integers(-60, 60, size=rows).astype(np.int32), type=pa.date32()),
-        "l_receiptdate": pa.array(ship + rng.integers(1, 31, size=rows).astype(np.int32), type=pa.date32()),
-        "l_shipinstruct": _dict_strings(pa, rng, ["DELIVER IN PERSON", "COLLECT COD", "NONE",
-                                                  "TAKE BACK RETURN"], rows),
-        "l_shipmode": _dict_strings(pa, rng, ["REG AIR", "AIR", "RAIL", "SHIP", "TRUCK", "MAIL", "FOB"], rows),
-        "l_comment": pc.binary_join_element_wise(c1, c2, " "),
-    })
-    po.write_table(table, path, compression="zstd", stripe_size=stripe_mb << 20,
-                   dictionary_key_size_threshold=0.5, row_index_stride=10000)
-
-
-def make_c5(path, rows, stripe_mb):
-    import pyarrow as pa
-    import pyarrow.orc as po
-
-    rng = np.random.default_rng(5)
-
-    def lengths(n):
-        ln = rng.integers(0, 9, size=n)
-        null = rng.random(n) < 0.1
-        ln[null] = 0
-        off = np.concatenate([[0], np.cumsum(ln)]).astype(np.int32)
-        return off, null
-
-    off_a, null_a = lengths(rows)
-    na = int(off_a[-1])
-    vals = pa.array(rng.integers(-(1 << 31), 1 << 31, size=na).astype(np.int32), mask=rng.random(na) < 0.1)
-    a = pa.ListArray.from_arrays(pa.array(off_a), vals, mask=pa.array(null_a))
-    off_m, null_m = lengths(rows)
-    nm = int(off_m[-1])
-    keys = pa.DictionaryArray.from_arrays(pa.array(rng.integers(0, 16, size=nm).astype(np.int32)),
-                                          pa.array(["key%02d" % i for i in range(16)])).cast(pa.string())
-    items = pa.array(rng.integers(0, 1 << 20, size=nm).astype(np.int32), mask=rng.random(nm) < 0.1)
-    m = pa.MapArray.from_arrays(pa.array(off_m), keys, items, mask=pa.array(null_m))
-    s = pa.StructArray.from_arrays([a, m], names=["a", "m"], mask=pa.array(rng.random(rows) < 0.1))
-    po.write_table(pa.table({"s": s}), path, compression="zstd", stripe_size=stripe_mb << 20,
-                   dictionary_key_size_threshold=1.0, row_index_stride=10000)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from workload_files import make_c3, make_c4, make_c5  # noqa: E402
 
 
 WORKLOADS = {

@@ -11,12 +11,26 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 # pyarrow (the file-level checker) resolves ORC writer zones under $TZDIR;
-# the image has no tzdata, so point it at the UTC zones of tests/tzdata.py
+# the image has no system tzdata: use the IANA files of the `tzdata` Python
+# package when it is installed, else the UTC zones of tests/tzdata.py
 if "TZDIR" not in os.environ:
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from tzdata import utc_tzdir
+    _tzd = None
+    try:
+        import importlib.util
 
-    os.environ["TZDIR"] = utc_tzdir()
+        _spec = importlib.util.find_spec("tzdata")
+        if _spec and _spec.origin:
+            _cand = os.path.join(os.path.dirname(_spec.origin), "zoneinfo")
+            if os.path.exists(os.path.join(_cand, "GMT")):
+                _tzd = _cand
+    except Exception:
+        _tzd = None
+    if _tzd is None:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from utc_zones import utc_tzdir
+
+        _tzd = utc_tzdir()
+    os.environ["TZDIR"] = _tzd
 
 
 def pytest_configure(config):

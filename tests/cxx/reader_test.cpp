@@ -1,12 +1,23 @@
 // Reference-style host program over the C++ RowReader adapter
-// (orc_amd/csrc/GpuRowReader.hh): reads every stripe of an ORC file through
-// Reader / RowReader::next(ColumnVectorBatch&) the way orc-contents does
-// (tools/src/FileContents.cc) and prints one JSON object per row, so the
-// Python test can compare it with pyarrow's rows.
+// (orc_amd/csrc/GpuRowReader.hh): reads an ORC file through Reader /
+// RowReader::next(ColumnVectorBatch&) the way tools/test/TestMatch.cc
+// (Contents) and orc-contents (tools/src/FileContents.cc) do, printing one
+// row per line in the reference ColumnPrinter's JSON shape
+// (c++/src/ColumnPrinter.cc) so the Python test can compare every line with
+// examples/expected/*.jsn.gz.
 //
-//   reader_test <file.orc>
+//   reader_test <file.orc> [--batch N] [--seek r1,r2,...] [--range OFF LEN] [--lazy] [--include id,...]
+//
+// --seek: for each row r, seekToRow(r) then one next(); prints "#seek r <getRowNumber>"
+//         before the batch's rows.
+// Every batch is checked against the contract: numElements <= capacity and
+// getRowNumber() == the batch's first row; the program exits non-zero when
+// it is broken or when the rows read differ from the file's row count.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
 #include <string>
 
 #include "../../orc_amd/csrc/GpuRowReader.hh"
@@ -31,6 +42,7 @@ static std::string json_str(const char* p, int64_t n) {
   return s + "\"";
 }
 
+// DecimalColumnPrinter: every scale digit, no quotes
 static std::string decimal_str(__int128 v, int32_t scale) {
   const bool neg = v < 0;
   unsigned __int128 m = neg ? (unsigned __int128)(-(v + 1)) + 1 : (unsigned __int128)v;
@@ -41,27 +53,68 @@ static std::string decimal_str(__int128 v, int32_t scale) {
   } while (m);
   while ((int32_t)digits.size() <= scale) digits.insert(digits.begin(), '0');
   if (scale > 0) digits.insert(digits.end() - scale, '.');
-  return "\"" + std::string(neg ? "-" : "") + digits + "\"";
+  return std::string(neg ? "-" : "") + digits;
 }
 
-static std::string value(const ColumnVectorBatch& b, uint64_t i) {
+// DateColumnPrinter: days since the epoch -> "YYYY-MM-DD" (proleptic Gregorian)
+static std::string date_str(int64_t days) {
+  int64_t z = days + 719468;
+  const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+  const int64_t doe = z - era * 146097;
+  const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+  int64_t y = yoe + era * 400;
+  const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+  const int64_t mp = (5 * doy + 2) / 153;
+  const int64_t d = doy - (153 * mp + 2) / 5 + 1;
+  const int64_t mo = mp < 10 ? mp + 3 : mp - 9;
+  if (mo <= 2) ++y;
+  char b[32];
+  snprintf(b, sizeof b, "\"%04lld-%02lld-%02lld\"", (long long)y, (long long)mo, (long long)d);
+  return b;
+}
+
+// TimestampColumnPrinter (ColumnPrinter.cc:668-700)
+static std::string timestamp_str(int64_t secs, int64_t nanos) {
+  time_t t = (time_t)secs;
+  struct tm tmv;
+  gmtime_r(&t, &tmv);
+  char buf[32];
+  strftime(buf, sizeof buf, "%Y-%m-%d %H:%M:%S", &tmv);
+  int zero = 0;
+  if (nanos == 0) zero = 8;
+  else
+    while (nanos % 10 == 0) {
+      nanos /= 10;
+      ++zero;
+    }
+  const std::string num = std::to_string(nanos);
+  std::string r = std::string("\"") + buf + ".";
+  for (int i = 0; i < 9 - zero - (int)num.size(); ++i) r += '0';
+  return r + num + "\"";
+}
+
+static std::string value(const ColumnVectorBatch& b, uint64_t i, const std::vector<std::string>* names = nullptr);
+
+static std::string value(const ColumnVectorBatch& b, uint64_t i, const std::vector<std::string>* names) {
   if (b.hasNulls && !b.notNull[i]) return "null";
   if (auto* l = dynamic_cast<const LongVectorBatch*>(&b)) {
     if (b.kind == ORCG_TYPE_BOOLEAN) return l->data[i] ? "true" : "false";
+    if (b.kind == ORCG_TYPE_DATE) return date_str(l->data[i]);
     return std::to_string(l->data[i]);
   }
   if (auto* d = dynamic_cast<const DoubleVectorBatch*>(&b)) {
     if (std::isnan(d->data[i])) return "NaN";
     if (std::isinf(d->data[i])) return d->data[i] > 0 ? "Infinity" : "-Infinity";
+    // DoubleColumnPrinter (ColumnPrinter.cc:345-353): %.7g for FLOAT, %.14g for DOUBLE
     char buf[64];
-    snprintf(buf, sizeof buf, "%.17g", d->data[i]);
+    snprintf(buf, sizeof buf, b.kind == ORCG_TYPE_FLOAT ? "%.7g" : "%.14g", d->data[i]);
     return buf;
   }
   if (auto* s = dynamic_cast<const StringVectorBatch*>(&b)) {
     if (b.kind == ORCG_TYPE_BINARY) {
       std::string r = "[";
       for (int64_t k = 0; k < s->length[i]; ++k)
-        r += (k ? "," : "") + std::to_string((unsigned char)s->data[i][k]);
+        r += (k ? ", " : "") + std::to_string((unsigned char)s->data[i][k]);
       return r + "]";
     }
     return json_str(s->data[i], s->length[i]);
@@ -72,56 +125,142 @@ static std::string value(const ColumnVectorBatch& b, uint64_t i) {
     const __int128 v = (__int128)(((unsigned __int128)(uint64_t)x.highbits << 64) | x.lowbits);
     return decimal_str(v, d128->scale);
   }
-  if (auto* t = dynamic_cast<const TimestampVectorBatch*>(&b))
-    return "[" + std::to_string(t->data[i]) + "," + std::to_string(t->nanoseconds[i]) + "]";
+  if (auto* t = dynamic_cast<const TimestampVectorBatch*>(&b)) return timestamp_str(t->data[i], t->nanoseconds[i]);
   if (auto* lb = dynamic_cast<const ListVectorBatch*>(&b)) {
     std::string r = "[";
     for (int64_t k = lb->offsets[i]; k < lb->offsets[i + 1]; ++k)
-      r += (k > lb->offsets[i] ? "," : "") + value(*lb->elements, (uint64_t)k);
-    return r + "]";
-  }
-  if (auto* sb = dynamic_cast<const StructVectorBatch*>(&b)) {  // nested struct: its field values in order
-    std::string r = "[";
-    for (size_t f = 0; f < sb->fields.size(); ++f) r += (f ? "," : "") + value(*sb->fields[f], i);
+      r += (k > lb->offsets[i] ? ", " : "") + value(*lb->elements, (uint64_t)k);
     return r + "]";
   }
   if (auto* mb = dynamic_cast<const MapVectorBatch*>(&b)) {
     std::string r = "[";
     for (int64_t k = mb->offsets[i]; k < mb->offsets[i + 1]; ++k)
-      r += std::string(k > mb->offsets[i] ? "," : "") + "[" + value(*mb->keys, (uint64_t)k) + "," +
-           value(*mb->elements, (uint64_t)k) + "]";
+      r += std::string(k > mb->offsets[i] ? ", " : "") + "{\"key\": " + value(*mb->keys, (uint64_t)k) +
+           ", \"value\": " + value(*mb->elements, (uint64_t)k) + "}";
     return r + "]";
+  }
+  if (auto* ub = dynamic_cast<const UnionVectorBatch*>(&b)) {
+    const unsigned tag = ub->tags[i];
+    return "{\"tag\": " + std::to_string(tag) + ", \"value\": " + value(*ub->children[tag], ub->offsets[i]) + "}";
+  }
+  if (auto* sb = dynamic_cast<const StructVectorBatch*>(&b)) {
+    std::string r = "{";
+    for (size_t f = 0; f < sb->fields.size(); ++f) {
+      const std::string nm = names ? (*names)[f] : "f" + std::to_string(f);
+      r += (f ? ", " : "") + json_str(nm.data(), (int64_t)nm.size()) + ": " + value(*sb->fields[f], i);
+    }
+    return r + "}";
   }
   return "null";
 }
 
+// selected field names of every struct in the type tree, by type id
+static void names_of(const Reader& r, uint32_t id, std::vector<std::vector<std::string>>& out) {
+  if (r.getType(id).kind == ORCG_TYPE_STRUCT) out[id] = r.getSelectedFieldNames(id);
+  for (uint32_t s : r.getSubtypes(id)) names_of(r, s, out);
+}
+
+static std::vector<std::vector<std::string>> g_names;
+
+// value() with nested struct field names (walks the batch tree alongside the type tree)
+static std::string row(const Reader& r, uint32_t id, const ColumnVectorBatch& b, uint64_t i) {
+  if (b.hasNulls && !b.notNull[i]) return "null";
+  const auto subs = r.getType(id).kind == ORCG_TYPE_STRUCT ? r.getSelectedSubtypes(id) : r.getSubtypes(id);
+  if (auto* sb = dynamic_cast<const StructVectorBatch*>(&b)) {
+    std::string s = "{";
+    for (size_t f = 0; f < sb->fields.size(); ++f) {
+      const std::string& nm = g_names[id][f];
+      s += (f ? ", " : "") + json_str(nm.data(), (int64_t)nm.size()) + ": " + row(r, subs[f], *sb->fields[f], i);
+    }
+    return s + "}";
+  }
+  if (auto* lb = dynamic_cast<const ListVectorBatch*>(&b)) {
+    std::string s = "[";
+    for (int64_t k = lb->offsets[i]; k < lb->offsets[i + 1]; ++k)
+      s += (k > lb->offsets[i] ? ", " : "") + row(r, subs[0], *lb->elements, (uint64_t)k);
+    return s + "]";
+  }
+  if (auto* mb = dynamic_cast<const MapVectorBatch*>(&b)) {
+    std::string s = "[";
+    for (int64_t k = mb->offsets[i]; k < mb->offsets[i + 1]; ++k)
+      s += std::string(k > mb->offsets[i] ? ", " : "") + "{\"key\": " + row(r, subs[0], *mb->keys, (uint64_t)k) +
+           ", \"value\": " + row(r, subs[1], *mb->elements, (uint64_t)k) + "}";
+    return s + "]";
+  }
+  if (auto* ub = dynamic_cast<const UnionVectorBatch*>(&b)) {
+    const unsigned tag = ub->tags[i];
+    return "{\"tag\": " + std::to_string(tag) + ", \"value\": " + row(r, subs[tag], *ub->children[tag], ub->offsets[i]) +
+           "}";
+  }
+  return value(b, i);
+}
+
 int main(int argc, char** argv) {
-  if (argc != 2) {
-    fprintf(stderr, "usage: %s <file.orc>\n", argv[0]);
+  if (argc < 2) {
+    fprintf(stderr, "usage: %s <file.orc> [--batch N] [--seek r1,r2,...] [--range OFF LEN] [--lazy] [--include ids]\n",
+            argv[0]);
     return 2;
+  }
+  uint64_t cap = 1024;
+  std::vector<uint64_t> seeks;
+  RowReaderOptions opts;
+  bool ranged = false;
+  for (int a = 2; a < argc; ++a) {
+    if (!strcmp(argv[a], "--batch") && a + 1 < argc) cap = strtoull(argv[++a], nullptr, 10);
+    else if (!strcmp(argv[a], "--lazy")) opts.setEnableLazyDecoding(true);
+    else if (!strcmp(argv[a], "--include") && a + 1 < argc) {
+      std::list<uint64_t> ids;
+      char* p = argv[++a];
+      while (*p) {
+        ids.push_back(strtoull(p, &p, 10));
+        if (*p == ',') ++p;
+      }
+      opts.include(ids);
+    }
+    else if (!strcmp(argv[a], "--range") && a + 2 < argc) {
+      opts.range(strtoull(argv[a + 1], nullptr, 10), strtoull(argv[a + 2], nullptr, 10));
+      a += 2;
+      ranged = true;
+    } else if (!strcmp(argv[a], "--seek") && a + 1 < argc) {
+      char* p = argv[++a];
+      while (*p) {
+        seeks.push_back(strtoull(p, &p, 10));
+        if (*p == ',') ++p;
+      }
+    }
   }
   try {
     Context ctx(0);
     Reader reader(ctx, argv[1]);
-    std::vector<std::string> names;
-    const auto subs = reader.getSubtypes(0);
-    for (size_t i = 0; i < subs.size(); ++i) names.push_back(reader.getFieldName(0, (uint32_t)i));
-    auto rows = reader.createRowReader();
-    auto batch = rows->createRowBatch();
-    uint64_t total = 0;
-    while (rows->next(*batch)) {
-      const auto& root = dynamic_cast<const StructVectorBatch&>(*batch);
-      for (uint64_t i = 0; i < batch->numElements; ++i) {
-        std::string line = "{";
-        for (size_t f = 0; f < names.size(); ++f)
-          line += (f ? ", " : "") + json_str(names[f].data(), (int64_t)names[f].size()) + ": " +
-                  value(*root.fields[f], i);
-        puts((line + "}").c_str());
+    auto rows = reader.createRowReader(opts);
+    g_names.assign(orcg_reader_num_types(reader.get()), {});
+    names_of(reader, 0, g_names);
+    auto batch = rows->createRowBatch(cap);
+    if (!seeks.empty()) {
+      for (uint64_t s : seeks) {
+        rows->seekToRow(s);
+        const bool more = rows->next(*batch);
+        printf("#seek %llu %llu %llu\n", (unsigned long long)s, (unsigned long long)rows->getRowNumber(),
+               (unsigned long long)(more ? batch->numElements : 0));
+        if (more && (batch->numElements > cap || rows->getRowNumber() != s)) return 3;
+        for (uint64_t i = 0; more && i < batch->numElements; ++i) puts(row(reader, 0, *batch, i).c_str());
       }
+      return 0;
+    }
+    uint64_t total = 0;
+    bool first = true;
+    while (rows->next(*batch)) {
+      if (batch->numElements > cap) return 3;
+      if (!ranged && rows->getRowNumber() != total) return 4;
+      if (ranged && first) printf("#first %llu\n", (unsigned long long)rows->getRowNumber());
+      first = false;
+      for (uint64_t i = 0; i < batch->numElements; ++i) puts(row(reader, 0, *batch, i).c_str());
       total += batch->numElements;
     }
-    fprintf(stderr, "rows %llu\n", (unsigned long long)total);
-    return total == reader.getNumberOfRows() ? 0 : 1;
+    fprintf(stderr, "rows %llu row_number %llu\n", (unsigned long long)total,
+            (unsigned long long)rows->getRowNumber());
+    if (ranged) return 0;
+    return total == reader.getNumberOfRows() && rows->getRowNumber() == total ? 0 : 1;
   } catch (const std::exception& e) {
     fprintf(stderr, "error: %s\n", e.what());
     return 1;

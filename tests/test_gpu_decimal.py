@@ -173,7 +173,7 @@ def test_decimal_file_matches_reference_expected_output():
 
 def test_pyarrow_written_decimals_and_timestamps(tmp_path):
     pa = pytest.importorskip("pyarrow")
-    from tzdata import utc_tzdir
+    from utc_zones import utc_tzdir
 
     os.environ["TZDIR"] = utc_tzdir()
     import pyarrow.orc as po

@@ -1,0 +1,185 @@
+"""RowReader on the GPU decode, against the reference's own expected output.
+
+Mirrors tools/test/TestMatch.cc:123-150 (Contents): createRowBatch(1024),
+next(batch) until it returns false, getRowNumber() == rows read before the
+batch, every row equal to examples/expected/<file>.jsn.gz (ColumnPrinter
+output), getRowNumber() == rowCount at the end. Plus the batch contract at
+other capacities (batches never exceed the capacity nor span a stripe:
+RowReaderImpl::next, c++/src/Reader.cc:1392-1442), seekToRow at row-group
+and stripe edges (:428-499), range(offset, length) stripe selection
+(:337-345) and lazy dictionary decoding (nextEncoded, ColumnReader.cc:596-607).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import orc_amd
+from conftest import load_golden
+from file_parity import expected_json, path, printer_equal, to_printer_form
+
+pytestmark = pytest.mark.gpu
+
+TESTMATCH = [d for d in load_golden("testmatch.json")
+             if os.path.exists(path(d["file"])) and expected_json(d["file"].replace(
+                 "demo-11-zlib", "demo-12-zlib")) is not None]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return orc_amd.Context(0)
+
+
+def _decodable(reader, batch):
+    """Top-level fields the GPU path decodes in this batch (TIMESTAMP columns
+    of writers in a zone other than UTC and Hive 0.11 decimals are not)."""
+    root = reader.types[0]
+    if root.kind != 12:
+        return None
+
+    def ok(tid):
+        return tid in batch.columns and all(ok(s) for s in reader.types[tid].subtypes)
+    return [n for n, s in zip(root.field_names, root.subtypes) if ok(s)]
+
+
+def _check_rows(reader, batch, want_rows, first, where):
+    fields = _decodable(reader, batch)
+    if fields is None and 0 not in batch.columns:
+        return None  # a non-struct root the GPU path does not decode (a non-UTC timestamp)
+    got = batch.to_pylist(fields)
+    for i, g in enumerate(got):
+        w = want_rows[first + i]
+        if fields is not None:
+            w = {k: w[k] for k in fields}
+        assert printer_equal(w, to_printer_form(g)), "%s row %d: %r vs %r" % (where, first + i, w, g)
+    return fields
+
+
+@pytest.mark.parametrize("d", TESTMATCH, ids=lambda d: d["file"])
+def test_contents_match_reference_expected_output(ctx, d):
+    name = d["file"]
+    want = expected_json(name.replace("demo-11-zlib", "demo-12-zlib"))
+    r = orc_amd.Reader(path(name), ctx)
+    rr = r.create_row_reader()
+    assert rr.get_row_number() == (1 << 64) - 1 or d["rows"] == 0 or r.num_stripes == 0
+    batch = rr.create_row_batch(1024)
+    rows = 0
+    decodable = None
+    while rr.next(batch):
+        assert rr.get_row_number() == rows
+        assert 0 < batch.num_elements <= 1024
+        decodable = _check_rows(r, batch, want, rows, name)
+        rows += batch.num_elements
+    assert rows == d["rows"] == len(want)
+    assert rr.get_row_number() == d["rows"]
+    if r.types[0].kind == 12 and d["rows"]:
+        assert decodable, "%s: no decodable column" % name
+
+
+@pytest.mark.parametrize("capacity", [1, 1000, 1024, 5000])
+@pytest.mark.parametrize("name", ["TestOrcFile.testSeek.orc", "TestOrcFile.testMemoryManagementV11.orc",
+                                  "nulls-at-end-snappy.orc"])
+def test_batches_respect_capacity_and_stripes(ctx, name, capacity):
+    r = orc_amd.Reader(path(name), ctx)
+    want = expected_json(name)
+    bounds = np.cumsum([0] + [r.stripe(s)["num_rows"] for s in range(r.num_stripes)])
+    rr = r.create_row_reader()
+    b = rr.create_row_batch(capacity)
+    rows = 0
+    # capacity 1 over a whole file is slow: check the first 3,000 rows there
+    limit = 3000 if capacity == 1 else None
+    while (limit is None or rows < limit) and rr.next(b):
+        n = b.num_elements
+        assert 0 < n <= capacity
+        s = int(np.searchsorted(bounds, rows, side="right") - 1)
+        assert rows + n <= bounds[s + 1], "batch spans a stripe"
+        assert rr.get_row_number() == rows
+        _check_rows(r, b, want, rows, name)
+        rows += n
+    if limit is None:
+        assert rows == r.num_rows and not rr.next(b) and rr.get_row_number() == r.num_rows
+
+
+def test_seek_to_row_at_row_group_and_stripe_edges(ctx):
+    """TestOrcFile.testSeek.orc: 32,768 rows, 7 stripes, row index stride 1,000."""
+    name = "TestOrcFile.testSeek.orc"
+    r = orc_amd.Reader(path(name), ctx)
+    want = expected_json(name)
+    firsts = np.cumsum([0] + [r.stripe(s)["num_rows"] for s in range(r.num_stripes)])
+    targets = [0, 1, 999, 1000, 1001, 4999, 5000, 12345, r.num_rows - 1]
+    targets += [int(x) for x in firsts[1:-1]] + [int(x) - 1 for x in firsts[1:-1]]
+    rr = r.create_row_reader()
+    b = rr.create_row_batch(37)
+    for t in targets + targets[::-1]:
+        rr.seek_to_row(t)
+        assert rr.get_row_number() == t
+        assert rr.next(b)
+        assert rr.get_row_number() == t
+        s = int(np.searchsorted(firsts, t, side="right") - 1)
+        assert b.num_elements == min(37, int(firsts[s + 1]) - t)
+        _check_rows(r, b, want, t, "seek %d" % t)
+    # past the end: no rows, row number = number of rows
+    rr.seek_to_row(r.num_rows)
+    assert not rr.next(b) and b.num_elements == 0
+    assert rr.get_row_number() == r.num_rows
+
+
+def test_range_selects_stripes_by_offset(ctx):
+    """RowReaderOptions::range(offset, length): the stripes whose first byte
+    lies in [offset, offset + length) (Reader.cc:337-345)."""
+    name = "TestOrcFile.testSeek.orc"
+    r = orc_amd.Reader(path(name), ctx)
+    want = expected_json(name)
+    st = [r.stripe(s) for s in range(r.num_stripes)]
+    firsts = np.cumsum([0] + [x["num_rows"] for x in st])
+    for lo, hi in [(0, 1), (2, 5), (6, 7), (1, 7)]:
+        off = st[lo]["offset"]
+        length = st[hi - 1]["offset"] - off + 1
+        rr = r.create_row_reader(offset=off, length=length)
+        b = rr.create_row_batch(4096)
+        rows = int(firsts[lo])
+        assert rr.get_row_number() == ((1 << 64) - 1 if lo == 0 else rows - 1)
+        while rr.next(b):
+            assert rr.get_row_number() == rows
+            _check_rows(r, b, want, rows, "range %d-%d" % (lo, hi))
+            rows += b.num_elements
+        assert rows == firsts[hi]
+        assert rr.get_row_number() == firsts[hi]
+    # an empty range reads nothing
+    rr = r.create_row_reader(offset=r.stripe(0)["offset"] + 1, length=1)
+    assert not rr.next(rr.create_row_batch(10))
+
+
+@pytest.mark.parametrize("name", ["demo-12-zlib.orc", "TestStringDictionary.testRowIndex.orc",
+                                  "TestOrcFile.testSeek.orc"])
+def test_lazy_dictionary_batches_match_eager(ctx, name):
+    """setEnableLazyDecoding: dictionary columns arrive as index + dictionary
+    (EncodedStringVectorBatch) and resolve to the same strings."""
+    r1 = orc_amd.Reader(path(name), ctx)
+    r2 = orc_amd.Reader(path(name), ctx)
+    a = r1.create_row_reader()
+    e = r2.create_row_reader(lazy_dictionary=True)
+    ba, be = a.create_row_batch(5000), e.create_row_batch(5000)
+    saw_encoded = False
+    while a.next(ba):
+        assert e.next(be) and be.num_elements == ba.num_elements
+        for tid, c in be.columns.items():
+            if c.index is not None and c.data is None:
+                saw_encoded = True
+        assert ba.to_pylist() == be.to_pylist()
+    assert not e.next(be)
+    # files with a dictionary-encoded string column hand out encoded batches
+    r3 = orc_amd.Reader(path(name), ctx)
+    b3 = r3.read_stripe(0)
+    has_dict = any(r3.types[t].kind in (7, 16, 17) and c.encoding in (1, 3) for t, c in b3.columns.items())
+    assert saw_encoded == has_dict
+
+
+def test_column_selection_in_row_reader(ctx):
+    r = orc_amd.Reader(path("TestOrcFile.test1.orc"), ctx)
+    rr = r.create_row_reader(include=["string1", "map"])
+    b = rr.create_row_batch(10)
+    assert rr.next(b)
+    ids = dict(zip(r.types[0].field_names, r.types[0].subtypes))
+    assert ids["string1"] in b.columns and ids["map"] in b.columns and ids["int1"] not in b.columns
+    assert [b.value(ids["string1"], i) for i in range(b.num_rows)] == ["hi", "bye"]

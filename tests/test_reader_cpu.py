@@ -91,3 +91,51 @@ def test_tail_with_wrapping_footer_length_is_rejected():
         bad = orc_file(b"", [], [type_msg(12)], 0, footer_length_override=flen)
         with pytest.raises(orc_amd.ParseError, match="Invalid tail size"):
             orc_amd.Reader(bad)
+
+
+@pytest.mark.parametrize("name", ["c4", "c5"])
+def test_workload_files_have_the_configured_shape(tmp_path, name):
+    """The configs[3] / configs[4] writers produce >= 3 stripes with a row
+    index and the encodings the parity tests rely on (RLEv2, dictionaries,
+    PRESENT streams); metadata only, no GPU."""
+    _pa()
+    from workload_files import make_c4, make_c5
+
+    p = str(tmp_path / (name + ".orc"))
+    {"c4": make_c4, "c5": make_c5}[name](p, 200_000, 1)
+    r = orc_amd.Reader(p)
+    assert r.num_rows == 200_000 and r.num_stripes >= 3 and r.row_index_stride == 10000
+    assert r.compression == "ZSTD"
+    kinds = [t.kind for t in r.types]
+    if name == "c4":
+        assert len(r.types[0].subtypes) == 16 and kinds.count(14) == 4 and kinds.count(15) == 3
+    else:
+        assert r.type_string() == "struct<s:struct<a:array<int>,m:map<string,int>>>"
+
+
+def _testmatch():
+    from conftest import load_golden
+    return [d for d in load_golden("testmatch.json") if os.path.exists(path(d["file"]))]
+
+
+@pytest.mark.parametrize("d", _testmatch(), ids=lambda d: d["file"])
+def test_metadata_matches_reference_testmatch(d):
+    """Reader metadata against the reference's TestMatch expectations
+    (tools/test/TestMatch.cc:98-121 Metadata: compression, compression size,
+    stripe count, row count, row index stride, content length, format
+    version, software version, user metadata, type string); no GPU."""
+    r = orc_amd.Reader(path(d["file"]))
+    assert r.compression == d["compression"]
+    assert r.compression_block_size == d["compression_size"]
+    assert r.num_stripes == d["stripes"]
+    assert r.num_rows == d["rows"]
+    assert r.row_index_stride == d["row_index_stride"]
+    assert r.content_length == d["content_length"]
+    assert r.format_version == d["format_version"]
+    assert r.software_version == d["software_version"]
+    assert r.type_string() == d["type"]
+    meta = r.metadata
+    assert set(meta) == set(d["metadata"])
+    for k, v in d["metadata"].items():
+        assert meta[k] == bytes.fromhex(v), k
+    assert "foo" not in meta
