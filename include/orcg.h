@@ -283,12 +283,8 @@ int orcg_rlev2_encode_runs(const int64_t* values, uint64_t n, int is_signed, con
                            const uint32_t* lengths, uint64_t nruns, uint8_t* dst, uint64_t dst_cap,
                            uint64_t* out_len, uint64_t* run_offsets);
 
-/* ---- measurement ----------------------------------------------------------
- * Roofline calibration: a device copy of `bytes` (multiple of 1 KB) in the
- * access shapes the decoder can use (mode 0: 16 B/lane loads + stores;
- * 1: 16 B + non-temporal stores; 2: 8 B + non-temporal stores; 3: 8 B + 8 B).
- * Asynchronous on the context stream. Not part of the decode path. */
-int orcg_probe_copy(orcg_ctx* ctx, const void* d_src, void* d_dst, uint64_t bytes, int mode);
+/* (Roofline calibration copies, orcg_probe_copy, live only in the A/B build
+ * liborcgpu_ab.so: orc_amd/csrc/probe_kernels.hip.) */
 
 #ifdef __cplusplus
 }

@@ -97,10 +97,12 @@ SIGNATURES = [
     ("orcg_decimal_decode_device", [vp, vp, u64, vp, u64, ctypes.c_uint32, i32, vp], i32),
     ("orcg_timestamp_decode_device", [vp, vp, vp, u64, ctypes.c_int64], i32),
     ("orcg_decode_integer_column", [vp, vp, u64, vp, u64, i32, u64, vp, vp], i32),
-    ("orcg_probe_copy", [vp, vp, vp, u64, i32], i32),
     ("orcg_rlev2_encode_direct", [vp, u64, i32, i32, vp, u64, ctypes.POINTER(u64), u64, vp], i32),
     ("orcg_rlev2_encode_runs", [vp, u64, i32, vp, vp, u64, vp, u64, ctypes.POINTER(u64), vp], i32),
 ]
+
+# symbols of the A/B build (liborcgpu_ab.so, ORCG_LIB) only
+AB_SIGNATURES = [("orcg_probe_copy", [vp, vp, vp, u64, i32], i32)]
 
 _lib = None
 
@@ -192,6 +194,11 @@ def load():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
+    for name, args, res in AB_SIGNATURES:  # present in the A/B build only
+        f = getattr(L, name, None)
+        if f is not None:
+            f.argtypes = args
+            f.restype = res
     _lib = L
     return L
 

@@ -9,11 +9,17 @@ CSRC = os.path.join(HERE, "csrc")
 # ORCG_PHASE_PROF=1 builds the phase-profiling variant (kernel cycle counters,
 # scripts/phase_prof.py) as liborcgpu_prof.so next to the product library.
 PROF = os.environ.get("ORCG_PHASE_PROF", "") == "1"
-OUT = os.path.join(HERE, "liborcgpu_prof.so" if PROF else "liborcgpu.so")
-OBJ = os.path.join(HERE, "build_prof" if PROF else "build")
+# ORCG_AB=1 builds the A/B variant (every tuning instance of the RLEv2 kernel,
+# RLEv2 variants 8-24, and the device copy probes; scripts/ab_rlev2.py) as
+# liborcgpu_ab.so; the product library carries only the default's instances.
+AB = os.environ.get("ORCG_AB", "") == "1"
+OUT = os.path.join(HERE, "liborcgpu_prof.so" if PROF else ("liborcgpu_ab.so" if AB else "liborcgpu.so"))
+OBJ = os.path.join(HERE, "build_prof" if PROF else ("build_ab" if AB else "build"))
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "probe_kernels.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "decimal_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "decimal_api.cpp", "encoder.cpp"]
+SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "decimal_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "decimal_api.cpp", "encoder.cpp"]
+if PROF or AB:
+    SOURCES.append("probe_kernels.hip")
 HEADERS = ["orcg_internal.hh", "rlev2_device.hh", "orc_file.hh", os.path.join("..", "..", "include", "orcg.h"),
            os.path.join("..", "..", "include", "orcg_reader.h")]
 
@@ -21,6 +27,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-result", "-Wno-unused-value"]
 if PROF:
     FLAGS.append("-DORCG_PHASE_PROF")
+if PROF or AB:
+    FLAGS.append("-DORCG_AB_VARIANTS")
 
 
 def _mtime(p):

@@ -216,6 +216,7 @@ void orcg_ctx_destroy(orcg_ctx* c) {
     if (c->d_scratch[i]) hipFree(c->d_scratch[i]);
   if (c->h_pinned) hipHostFree(c->h_pinned);
   if (c->d_err) hipFree(c->d_err);
+  if (c->d_defer) hipFree(c->d_defer);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
 }

@@ -48,6 +48,9 @@ struct Ctx {
   void* h_pinned = nullptr;
   size_t pinned_cap = 0;
   int rlev2_variant = ORCG_RLEV2_TILED;  // which RLEv2 kernel to launch
+  void* d_defer = nullptr;  // RLEv2 short-run segment queue (rlev2_tiled.hip defer_queue)
+  uint64_t defer_cap = 0;
+  uint64_t defer_seq = 0;  // launches that used the queue (count parity)
 };
 
 int set_error(Ctx* ctx, int status, const std::string& msg);
@@ -65,7 +68,7 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
 
 // RLEv2 kernel variants a context accepts (orcg_rlev2_variants): 0 default,
 // 1 wave-walk, and pins of single tiled instances (launch_rlev2_tiled).
-constexpr int kMaxRlev2Variant = 20;
+constexpr int kMaxRlev2Variant = 24;
 bool rlev2_variant_valid(int v);
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,

@@ -170,6 +170,8 @@ __global__ __launch_bounds__(256) void copy_reg_kernel(const uint8_t* __restrict
 
 using namespace orcg;
 
+// A/B build only (not declared in include/orcg.h): device copies in the
+// decoder's access shapes, the roofline references of scripts/ab_rlev2.py.
 extern "C" int orcg_probe_copy(orcg_ctx* c, const void* d_src, void* d_dst, uint64_t bytes, int mode) {
   if (!c || !d_src || !d_dst || (bytes % 1024) != 0 || mode < 0 || mode > 11) return ORCG_INVALID_ARGUMENT;
   (void)hipSetDevice(c->device);

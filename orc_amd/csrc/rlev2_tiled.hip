@@ -23,6 +23,8 @@
 //    run tables, one raw s_barrier per window. The producer never stores and
 //    the consumers never wait on vmcnt, so output stores stay in flight across
 //    windows.
+#include <type_traits>
+
 #include "rlev2_device.hh"
 
 namespace orcg {
@@ -494,8 +496,8 @@ __device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint
 // Wave-uniform header walk over the window [wpos, wpos + kWin): records runs
 // starting at pos.. into (run_off, run_val) until the next run starts past
 // kWin - kMaxRun, leaves the segment, or the table is full.
-template <uint32_t kWin, uint32_t kCap, bool kT4 = false>
-__device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_off, uint32_t* run_val,
+template <uint32_t kWin, uint32_t kCap, bool kT4 = false, typename OffT = uint32_t>
+__device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, uint32_t* run_val,
                                            uint64_t wpos, uint64_t pos, uint64_t vi, uint64_t seg_end,
                                            uint64_t src_len, uint64_t value_end, int is_signed,
                                            unsigned long long* err, int lane, uint32_t lim = kWin,
@@ -518,7 +520,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, uint32_t* run_of
       break;
     }
     if (lane == 0) {
-      run_off[n] = lp;
+      run_off[n] = (OffT)lp;
       run_val[n] = (uint32_t)(v - vi);
       // expanding waves may claim the run as soon as it is published
       if (pub) __hip_atomic_store(pub, n + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -746,6 +748,265 @@ __device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint3
   return DenseResult{uni(total), uni(s_ctl[3]), uni(s_ctl[1]), uni(s_ctl[2])};
 }
 
+// ---- dense mode v2 -----------------------------------------------------
+// The same contract as dense_discover, restructured for the CDNA issue model
+// (the v1 code spent ~3.7 SALU instructions per decoded value on exec-mask
+// bookkeeping of divergent branches):
+//  * the speculative header parse at every position is branch-free (all
+//    kinds computed, selected by kind) and the in-block DP lives in
+//    registers, indexed at compile time (select chains), not through LDS;
+//  * PATCHED_BASE headers and DELTA varints over 10 bytes are "unknown" to
+//    the DP: a block whose path meets one re-walks exactly (checked_run), as
+//    v1 does for corrupt runs; such a block also ends the pass;
+//  * the chain keeps each thread's 8 successors in registers and one u16 LDS
+//    slot per position (single-buffered: a barrier on each side of the
+//    write); marks propagate only from threads holding a marked position;
+//  * a block's runs come from a forward pass over the DP registers (no
+//    header re-parse), appended to the run table with predicated writes.
+constexpr uint32_t kDpUnknown = 0x80000000u;
+
+// FBSToBitWidthMap without a branch (RLEV2Util.cc:24-26)
+__device__ __forceinline__ uint32_t fbs_width_nb(uint32_t code) {
+  const uint32_t hi = (uint32_t)((0x40383028201E1C1Aull >> (8 * ((code - 24u) & 7u))) & 0xffu);
+  return code < 24 ? code + 1 : hi;
+}
+
+template <typename OffT>
+__device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT* s_off, uint32_t* s_val,
+                                                       uint16_t* s_nxt, uint32_t* s_mark, uint32_t* s_ctl,
+                                                       uint64_t wpos, uint32_t sb, uint32_t lim, uint64_t vi,
+                                                       uint64_t seg_end, uint64_t src_len, uint64_t value_end,
+                                                       uint32_t need, int is_signed, unsigned long long* err,
+                                                       int tid
+#ifdef ORCG_PHASE_PROF
+                                                       , uint64_t& prof_last_
+#endif
+) {
+  const int wave = tid / kWave, lane = tid % kWave;
+  const uint32_t lo = (uint32_t)tid * kBlk, hi = lo + kBlk;
+  __builtin_amdgcn_s_setprio(2);
+  // runs may not start at or past the segment end
+  {
+    const uint64_t sa = wpos + sb;
+    const uint64_t seg_room = seg_end > sa ? seg_end - sa : 0;
+    if (seg_room < lim) lim = (uint32_t)seg_room;
+  }
+  // (1) per position e of the block: ent[e] = exit (first run start past the
+  // block on the path from e) | values on the path << 15, or kDpUnknown;
+  // info (two positions per register): in-block successor (e + run bytes,
+  // 15 = past the block) | L << 4
+  uint32_t ent[kBlk], info2[kBlk / 2];
+  {
+    const uint32_t a0 = sb + lo, sh = a0 & 3u, w0 = a0 >> 2;
+    uint32_t b4[kBlk / 4 + 8];
+    {
+      uint32_t prev = win[w0];
+#pragma unroll
+      for (int i = 0; i < (int)kBlk / 4 + 8; ++i) {
+        const uint32_t nx = win[w0 + i + 1];
+        b4[i] = __builtin_amdgcn_alignbyte(nx, prev, sh);
+        prev = nx;
+      }
+    }
+    uint64_t term = 0;  // bit i: byte i < 0x80 (varint terminators)
+#pragma unroll
+    for (int i = 0; i < (int)kBlk / 4 + 8 && i < 16; ++i) {
+      const uint32_t m = (~b4[i] >> 7) & 0x01010101u;
+      term |= (uint64_t)((m * 0x10204080u) >> 28) << (4 * i);
+    }
+    auto B = [&](int i) -> uint32_t { return (b4[i >> 2] >> ((i & 3) * 8)) & 0xffu; };
+    // bytes from block byte 0 that a run may use: inside the stream, the
+    // segment and the loaded window
+    const uint64_t pblk = wpos + sb + lo;
+    const uint64_t lim_abs = src_len < seg_end ? src_len : seg_end;
+    const uint64_t r1 = lim_abs > pblk ? lim_abs - pblk : 0;
+    const uint32_t r2 = need > sb + lo ? need - (sb + lo) : 0u;
+    const uint32_t room0 = r1 < (uint64_t)r2 ? (uint32_t)r1 : r2;
+#pragma unroll
+    for (int e = (int)kBlk - 1; e >= 0; --e) {
+      const uint32_t fb = B(e), b1 = B(e + 1);
+      const uint32_t kind = fb >> 6, code = (fb >> 1) & 0x1fu;
+      const uint32_t W = fbs_width_nb(code);
+      const uint32_t L2 = ((fb & 1u) << 8 | b1) + 1u;
+      const uint32_t sr_bytes = 2u + ((fb >> 3) & 7u), sr_L = (fb & 7u) + 3u;
+      const uint32_t di_bytes = 2u + (W * L2 + 7u) / 8u;
+      const uint32_t Wd = code ? W : 0u;
+      const uint64_t t1 = term >> (e + 2);
+      const uint32_t n1 = t1 ? (uint32_t)__builtin_ctzll(t1) + 1u : 64u;
+      const uint64_t t2 = n1 < 32 ? t1 >> n1 : 0ull;
+      const uint32_t n2 = t2 ? (uint32_t)__builtin_ctzll(t2) + 1u : 64u;
+      const bool de_ok = n1 <= 10 && n2 <= 10 && !(Wd != 0 && L2 < 2);
+      const uint32_t de_bytes = 2u + n1 + n2 + (Wd ? (Wd * (L2 - 2u) + 7u) / 8u : 0u);
+      const uint32_t bytes = kind == 0 ? sr_bytes : (kind == 1 ? di_bytes : de_bytes);
+      const uint32_t L = kind == 0 ? sr_L : L2;
+      const uint32_t room = room0 > (uint32_t)e ? room0 - (uint32_t)e : 0u;
+      const bool ok = kind != 2 && (kind != 3 || de_ok) && bytes <= room;
+      const uint32_t nx = (uint32_t)e + bytes;
+      const uint32_t inf = (nx < 15u ? nx : 15u) | (L << 4);
+      if (e & 1) info2[e >> 1] = inf << 16;
+      else info2[e >> 1] |= inf;
+      uint32_t sel = lo + nx;  // the exit when the run leaves the block
+      bool past = true;
+#pragma unroll
+      for (int k = e + 2; k < (int)kBlk; ++k) {
+        if (nx == (uint32_t)k) {
+          sel = ent[k];
+          past = false;
+        }
+      }
+      const bool path_ok = past || !(sel & kDpUnknown);
+      ent[e] = (ok && path_ok) ? (past ? sel | (L << 15) : sel + (L << 15)) : kDpUnknown;
+    }
+  }
+  PROF_MARK(3);
+  // (2) the chain from slab position 0 by pointer doubling over two
+  // successor tables (read one, write the other: one barrier per level)
+  uint32_t na[kBlk];
+#pragma unroll
+  for (int e = 0; e < (int)kBlk; ++e) {
+    const uint32_t x = ent[e] & 0x7fffu;
+    na[e] = ((ent[e] & kDpUnknown) || x >= lim) ? (uint32_t)kSink : x;
+  }
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  auto put8 = [&](uint16_t* t) {
+    u4 w;
+    w.x = na[0] | na[1] << 16;
+    w.y = na[2] | na[3] << 16;
+    w.z = na[4] | na[5] << 16;
+    w.w = na[6] | na[7] << 16;
+    *(u4*)(t + lo) = w;
+  };
+  uint16_t* ta = s_nxt;
+  uint16_t* tb = s_nxt + kSlab;
+  put8(ta);
+  if (tid < (int)(kSlab / 32)) s_mark[tid] = tid == 0;  // position 0 starts the chain
+  __syncthreads();
+#pragma unroll 1
+  for (int lev = 0; lev < 8; ++lev) {
+    const uint32_t m8 = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
+    if (m8) {
+      // marked positions mark their successor (marks only grow, and every
+      // marked position is a chain element, so racing with this level's
+      // readers is harmless)
+#pragma unroll
+      for (int e = 0; e < (int)kBlk; ++e) {
+        const bool go = ((m8 >> e) & 1u) && na[e] != kSink;
+        const uint32_t n = go ? na[e] : 0u;
+        atomicOr(&s_mark[n >> 5], go ? 1u << (n & 31u) : 0u);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < (int)kBlk; ++e) {
+      const bool valid = na[e] != kSink;
+      const uint32_t v = ta[valid ? na[e] : lo + (uint32_t)e];
+      na[e] = valid ? v : (uint32_t)kSink;
+    }
+    put8(tb);
+    uint16_t* t = ta;
+    ta = tb;
+    tb = t;
+    __syncthreads();
+  }
+  PROF_MARK(4);
+  // (3) the block's entry, its runs (a forward pass over the DP registers),
+  // one combined scan of the values and run counts
+  const uint32_t mb = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
+  const bool has = mb != 0;
+  const uint32_t eb = has ? (uint32_t)__builtin_ctz(mb) : 0u;
+  uint32_t ee = ent[0];
+#pragma unroll
+  for (int k = 1; k < (int)kBlk; ++k) ee = eb == (uint32_t)k ? ent[k] : ee;
+  const bool exact = has && (ee & kDpUnknown);
+  uint32_t cnt = 0, pk_off = 0, cum = 0, p_end = ee & 0x7fffu;
+  uint64_t pk_val = 0;
+  bool stopped = false;
+  if (has && !exact) {
+    uint32_t reach = 1u << eb;
+#pragma unroll
+    for (int e = 0; e < (int)kBlk; ++e) {
+      const bool on = ((reach >> e) & 1u) && !stopped;
+      const bool st = on && lo + (uint32_t)e >= lim;
+      p_end = st ? lo + (uint32_t)e : p_end;
+      stopped = stopped || st;
+      const bool em = on && !st;
+      const uint32_t inf = (info2[e >> 1] >> ((e & 1) * 16)) & 0xffffu;
+      const uint32_t nx = inf & 15u, Le = inf >> 4;
+      pk_off |= em ? (uint32_t)e << (3 * cnt) : 0u;
+      pk_val |= em ? (uint64_t)cum << (16 * cnt) : 0ull;
+      cnt += em ? 1u : 0u;
+      reach |= (em && nx < kBlk) ? 1u << nx : 0u;
+      cum += em ? Le : 0u;
+    }
+  }
+  uint32_t* s_wsum = s_ctl + 4;  // [0..3] value totals, [4..7] run-count totals of the waves
+  const uint32_t vincl = wave_scan_u32(cum), cincl = wave_scan_u32(cnt);
+  if (lane == kWave - 1) {
+    s_wsum[wave] = vincl;
+    s_wsum[4 + wave] = cincl;
+  }
+  if (tid == 0) {
+    s_ctl[3] = 0;       // stop (corrupt run)
+    s_ctl[12] = kNone;  // first block whose walk stopped inside it
+    s_ctl[13] = 0;      // last block with an entry
+    s_ctl[14] = 0;      // runs of the exact-walk block
+  }
+  __syncthreads();
+  uint32_t vb = vincl - cum, base = cincl - cnt;
+  for (int w = 0; w < wave; ++w) {
+    vb += s_wsum[w];
+    base += s_wsum[4 + w];
+  }
+  uint32_t total = s_wsum[4] + s_wsum[5] + s_wsum[6] + s_wsum[7];
+  uint32_t v_end = vb + cum;
+  if (exact) {
+    // the path meets a run the DP cannot vouch for (it is the pass's last
+    // block with an entry): walk it exactly
+    uint32_t p = lo + eb, v = vb;
+    while (p < hi && p < lim && vi + v < value_end) {
+      Run r;
+      const uint32_t e = checked_run(win, sb + p, wpos, seg_end, src_len, need, is_signed, &r);
+      if (e != kErrNone) {
+        report(err, vi + v, e);
+        s_ctl[3] = 1;
+        break;
+      }
+      pk_off |= (p - lo) << (3 * cnt);
+      pk_val |= (uint64_t)(v - vb) << (16 * cnt);
+      ++cnt;
+      p += r.bytes;
+      v += r.L;
+    }
+    stopped = p < hi;
+    p_end = p;
+    v_end = v;
+    s_ctl[14] = cnt;
+  }
+  if (has) {
+    if (stopped) atomicMin(&s_ctl[12], (uint32_t)tid);
+    atomicMax(&s_ctl[13], (uint32_t)tid);
+  }
+  // the successor tables are dead: the run table may overwrite them
+  __syncthreads();
+  {
+    const uint32_t fin = s_ctl[12] != kNone ? s_ctl[12] : s_ctl[13];
+    if ((uint32_t)tid == fin) {
+      s_ctl[1] = p_end;
+      s_ctl[2] = v_end;
+    }
+  }
+  total += s_ctl[14];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+    if (k < cnt) {
+      s_off[base + k] = (OffT)(sb + lo + ((pk_off >> (3 * k)) & 7u));
+      s_val[base + k] = vb + (uint32_t)((pk_val >> (16 * k)) & 0xffffu);
+    }
+  __syncthreads();
+  PROF_MARK(5);
+  __builtin_amdgcn_s_setprio(0);
+  return DenseResult{uni(total), uni(s_ctl[3]), uni(s_ctl[1]), uni(s_ctl[2])};
+}
+
 // Value j of a short run (kind SHORT_REPEAT / DIRECT / DELTA) parsed at
 // window offset `hoff`; `acc` carries a variable-width DELTA run's |delta| sum.
 __device__ __forceinline__ uint64_t short_value(const uint32_t* win, const Run& r, uint32_t hoff, uint32_t j,
@@ -771,8 +1032,8 @@ __device__ __forceinline__ uint64_t short_value(const uint32_t* win, const Run& 
 // consecutive short runs (<= kStage values) are decoded one lane per run into
 // the wave's LDS stage and flushed with coalesced stores; any other run
 // (long, PATCHED_BASE) goes through expand_run.
-template <int kOpt, typename T>
-__device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nwords, const uint32_t* s_off,
+template <int kOpt, typename T, typename OffT>
+__device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nwords, const OffT* s_off,
                                              const uint32_t* s_val, uint64_t* stage, uint32_t r0, uint32_t r1,
                                              uint64_t vi, int is_signed, uint64_t value_begin, uint64_t value_end,
                                              T* dst, int lane) {
@@ -857,6 +1118,21 @@ struct DenseLds {
 template <>
 struct DenseLds<false> {};
 
+// Dense v2 LDS: the run table (u16 window offsets, u32 value offsets) shares
+// its bytes with the chain's single successor table (dead once the runs are
+// emitted); per-wave value stages; chain marks.
+struct Dense2Lds {
+  union {
+    struct {
+      uint16_t off[kDenseRuns];
+      uint32_t val[kDenseRuns];
+    } tab;
+    uint16_t nxt[2 * kSlab];
+  };
+  uint64_t stage[kThreads / kWave][kStage];
+  uint32_t mark[kSlab / 32];
+};
+
 template <bool kDense>
 __device__ __forceinline__ uint16_t* s_dense_nxt(DenseLds<kDense>& d) {
   if constexpr (kDense) return &d.nxt[0][0];
@@ -868,11 +1144,20 @@ __device__ __forceinline__ uint32_t* s_dense_mark(DenseLds<kDense>& d) {
   else return nullptr;
 }
 
-template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMinWaves, bool kDense = false>
+// Deferral (kDefer): a serial-walk instance (kDefer = 1) whose probe pass
+// finds short runs stops at the end of that pass and queues {segment, byte
+// offset, value index} in `defer_q` (two counts, then 3 words per entry);
+// the dense instance launched right after it (kDefer = 2) drains the queue
+// with a persistent grid, so a short-run segment never runs the one-wave
+// header walk, whatever the stream's overall density. Launches alternate
+// between the two counts (`defer_par`): the drain of launch k zeroes the
+// count launch k + 1 will use, one store instead of a grid-wide handshake.
+template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMinWaves, int kDense = 0, int kDefer = 0>
 __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint8_t* __restrict__ src, uint64_t src_len, int is_signed,
     const uint64_t* __restrict__ segtab, uint64_t nsegs, uint64_t rows_per_group,
-    uint64_t value_begin, uint64_t nvalues, T* __restrict__ dst, unsigned long long* err) {
+    uint64_t value_begin, uint64_t nvalues, T* __restrict__ dst, unsigned long long* err,
+    unsigned long long* __restrict__ defer_q, uint32_t defer_par) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
@@ -880,29 +1165,45 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   static_assert(!kDense || kChunk % kSlab == 0, "dense window chunk must be whole slabs");
   constexpr int kBufs = kPipe ? 2 : 1;
   static_assert(!(kDense && kPipe), "dense mode is a non-pipelined instance");
-  // run table capacity; in dense instances the slab DP table aliases it
+  // run table capacity; in dense v1 instances the slab DP table aliases it
   constexpr uint32_t kCap = kDense ? kDenseRuns : 512u;
   static_assert(!kDense || 2 * kCap >= kSlab, "DP table must fit the run table");
   static_assert(!kDense || kChunk >= kSlab, "window too small for a slab");
+  using OffT = typename std::conditional<kDense == 2, uint16_t, uint32_t>::type;
   __shared__ __attribute__((aligned(16))) uint32_t s_win[kBufs][kWin / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
-  __shared__ uint32_t s_tab[kBufs][2 * kCap];
-  __shared__ uint32_t s_ctl[kBufs][12];
+  __shared__ uint32_t s_ctl[kBufs][16];
   __shared__ uint32_t s_sync[2][2];  // serial passes: {published runs, claimed runs}, by pass parity
-  __shared__ DenseLds<kDense> s_dense;
-  uint32_t* s_off[kBufs];
+  __shared__ DenseLds<kDense == 1> s_dense;
+  OffT* s_off[kBufs];
   uint32_t* s_val[kBufs];
-  for (int b = 0; b < kBufs; ++b) {
-    s_off[b] = s_tab[b];
-    s_val[b] = s_tab[b] + kCap;
+  uint32_t* s_tab0 = nullptr;   // v1: the slab DP table (aliases the run table)
+  uint16_t* s_nxt2 = nullptr;   // v2: successor table, marks, stages
+  uint32_t* s_mark2 = nullptr;
+  uint64_t* s_stage2 = nullptr;
+  if constexpr (kDense == 2) {
+    __shared__ __attribute__((aligned(16))) Dense2Lds s_d2;
+    s_off[0] = s_d2.tab.off;
+    s_val[0] = s_d2.tab.val;
+    s_nxt2 = s_d2.nxt;
+    s_mark2 = s_d2.mark;
+    s_stage2 = &s_d2.stage[0][0];
+  } else {
+    __shared__ uint32_t s_tab[kBufs][2 * kCap];
+    for (int b = 0; b < kBufs; ++b) {
+      s_off[b] = s_tab[b];
+      s_val[b] = s_tab[b] + kCap;
+    }
+    s_tab0 = s_tab[0];
   }
 
-  const uint64_t g = blockIdx.x;
   const int tid = (int)threadIdx.x;
   const int wave = tid / kWave, lane = tid % kWave;
   const uint64_t value_end = value_begin + nvalues;
 
-  const uint64_t seg_start = segtab[2 * g];
-  uint64_t vi = kPositions ? g * rows_per_group - segtab[2 * g + 1] : segtab[2 * g + 1];
+  // one segment, from its start or (queued) from a byte offset / value index
+  auto run_segment = [&](const uint64_t g, const bool queued, const uint64_t q_pos, const uint64_t q_vi) {
+  const uint64_t seg_start = queued ? q_pos : segtab[2 * g];
+  uint64_t vi = queued ? q_vi : (kPositions ? g * rows_per_group - segtab[2 * g + 1] : segtab[2 * g + 1]);
   uint64_t seg_end = src_len;
   uint64_t v_next = ~0ull;
   if (g + 1 < nsegs) {
@@ -933,8 +1234,11 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   if constexpr (!kPipe) {
     uint64_t pwpos = ~0ull;  // previous window (stream offset) and its valid bytes
     uint32_t pneed = 0;
-    bool dense = false;      // wave-uniform mode of the next pass (dense instances only)
-    bool probe = true;       // the segment's first pass
+    // wave-uniform mode of the next pass (dense instances only): the
+    // segment's first pass is a short serial probe (32 runs in v1, 4 in v2)
+    // whose bytes per run pick the mode
+    bool dense = queued;
+    bool probe = !queued;
     while (pos < seg_end && vi < value_end) {
       const uint32_t wrel = (uint32_t)(pos - bias) & ~15u;
       const uint64_t wpos = bias + wrel;
@@ -995,20 +1299,33 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         if (was_dense) {
           const uint32_t sb = (uint32_t)(pos - wpos);
           const uint32_t lim = min(kSlab, kChunk - sb);
-          const DenseResult d =
-              dense_discover(s_win[0], s_tab[0], s_off[0], s_val[0], s_dense_nxt(s_dense), s_dense_mark(s_dense),
-                             s_ctl[0], wpos, sb, lim, vi, seg_end, src_len, value_end, need, is_signed, err, tid
+          DenseResult d;
+          if constexpr (kDense == 2) {
+            d = dense2_discover(s_win[0], s_off[0], s_val[0], s_nxt2, s_mark2, s_ctl[0], wpos, sb, lim, vi, seg_end,
+                                src_len, value_end, need, is_signed, err, tid
 #ifdef ORCG_PHASE_PROF
-                             , prof_last_
+                                , prof_last_
 #endif
-              );
+            );
+          } else if constexpr (kDense == 1) {
+            d = dense_discover(s_win[0], s_tab0, (uint32_t*)s_off[0], s_val[0], s_dense_nxt(s_dense),
+                               s_dense_mark(s_dense), s_ctl[0], wpos, sb, lim, vi, seg_end, src_len, value_end, need,
+                               is_signed, err, tid
+#ifdef ORCG_PHASE_PROF
+                               , prof_last_
+#endif
+            );
+          }
           n = d.n;
           stop = d.stop;
           dpos = d.dpos;
           dval = d.dval;
-          if constexpr (kDense) {
+          if constexpr (kDense != 0) {
+            uint64_t* stage;
+            if constexpr (kDense == 2) stage = s_stage2 + wave * kStage;
+            else stage = s_dense.stage[wave];
             const uint32_t r0 = (uint32_t)(((uint64_t)n * wave) / kWaves), r1 = (uint32_t)(((uint64_t)n * (wave + 1)) / kWaves);
-            dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], s_dense.stage[wave], r0, r1, vi, is_signed,
+            dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], stage, r0, r1, vi, is_signed,
                                value_begin, value_end, dst, lane);
           }
         } else {
@@ -1023,8 +1340,9 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             __builtin_amdgcn_s_setprio(3);
             // dense instances: a short first walk (the probe) measures the
             // stream's bytes per run before committing to a mode
-            const uint32_t cap = (kDense && probe) ? 32u : kCap;
-            const WalkResult w = walk<kWin, kCap, (kOpt & kOptT4) != 0>(s_win[0], s_off[0], s_val[0], wpos, pos, vi,
+            // probe pass: 32 runs (v1 dense), 4 (v2 dense), 8 (queueing serial)
+            const uint32_t cap = ((kDense || kDefer == 1) && probe) ? (kDense == 2 ? 4u : (kDefer == 1 ? 8u : 32u)) : kCap;
+            const WalkResult w = walk<kWin, kCap, (kOpt & kOptT4) != 0, OffT>(s_win[0], s_off[0], s_val[0], wpos, pos, vi,
                                                                     seg_end, src_len, value_end, is_signed, err,
                                                                     lane, need, cap, s_pub);
             if (lane == 0) {
@@ -1067,12 +1385,25 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         if (stop) return;
         pos += dpos;
         vi += dval;
+        const bool was_probe = probe;
         probe = false;
+        if constexpr (kDefer == 1) {
+          // a short-run segment: queue the rest for the dense instance
+          if (was_probe && n >= 8 && dpos / n < kToDense && pos < seg_end && vi < value_end) {
+            if (tid == 0) {
+              const unsigned long long slot = atomicAdd(&defer_q[defer_par], 1ull);
+              defer_q[2 + 3 * slot] = g;
+              defer_q[3 + 3 * slot] = pos;
+              defer_q[4 + 3 * slot] = vi;
+            }
+            return;
+          }
+        }
         if constexpr (kDense) {
           // hysteresis on the stream bytes per run of this pass
           if (n > 0) {
             const uint32_t bpr = dpos / n;
-            if (!dense && n >= 8 && bpr < kToDense) dense = true;
+            if (!dense && (n >= 8 || (was_probe && n >= 4)) && bpr < kToDense) dense = true;
             else if (dense && bpr >= kToSerial) dense = false;
           }
         }
@@ -1129,13 +1460,56 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   }
   if (tid == 0 && v_next != ~0ull && vi < value_end && vi != v_next) report(err, vi, kErrBadSegment);
   if (tid == 0 && v_next == ~0ull && vi < value_end) report(err, vi, kErrBadRead);  // stream ended early
+  };
+
+  if constexpr (kDefer == 2) {
+    // persistent drain of the queue; the next launch's count starts at 0
+    if (blockIdx.x == 0 && tid == 0) defer_q[defer_par ^ 1u] = 0;
+    const uint64_t count = uni64(defer_q[defer_par]);
+    for (uint64_t i = blockIdx.x; i < count; i += gridDim.x) {
+      run_segment(uni64(defer_q[2 + 3 * i]), true, uni64(defer_q[3 + 3 * i]), uni64(defer_q[4 + 3 * i]));
+      __syncthreads();  // LDS is reused by the next entry
+    }
+  } else {
+    run_segment(blockIdx.x, false, 0, 0);
+  }
 }
 
 }  // namespace
 
-bool rlev2_variant_valid(int v) { return v == 0 || v == 1 || (v >= 8 && v <= kMaxRlev2Variant); }
+// Variants (ctx->rlev2_variant, include/orcg.h): 0 = the density-adaptive
+// default; 2-5 pin one of the instances the default launches (the parity
+// tests run each); 1 = the wave-walk kernel (rlev2_kernels.hip). The
+// tuning experiments of the A/B sweeps (8-24) are compiled only into the A/B
+// build (ORCG_AB=1 python -m orc_amd.build -> liborcgpu_ab.so).
+bool rlev2_variant_valid(int v) {
+  if (v >= 0 && v <= 5) return true;
+#ifdef ORCG_AB_VARIANTS
+  if (v >= 8 && v <= kMaxRlev2Variant) return true;
+#endif
+  return false;
+}
 
-// Variants (ctx->rlev2_variant): 0 = default; 8.. = single instances.
+static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
+  // [0] count, [1] done, then {segment, byte offset, value index} per entry;
+  // both counts start at zero; each drain zeroes the count of the next launch
+  if (ctx->defer_cap < nsegs) {
+    if (ctx->d_defer) {
+      (void)hipStreamSynchronize(ctx->stream);
+      (void)hipFree(ctx->d_defer);
+      ctx->d_defer = nullptr;
+      ctx->defer_cap = 0;
+    }
+    const uint64_t cap = std::max<uint64_t>(nsegs, 4096);
+    int rc = hip_check(ctx, hipMalloc(&ctx->d_defer, (2 + 3 * cap) * 8), "hipMalloc defer queue");
+    if (!rc) rc = hip_check(ctx, hipMemsetAsync(ctx->d_defer, 0, 16, ctx->stream), "defer queue reset");
+    if (rc) return rc;
+    ctx->defer_cap = cap;
+  }
+  *out = (unsigned long long*)ctx->d_defer;
+  return ORCG_OK;
+}
+
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
@@ -1144,17 +1518,23 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   if (dst_bytes != 8 && dst_bytes != 4 && dst_bytes != 2)
     return set_error(ctx, ORCG_INVALID_ARGUMENT, "dst_bytes must be 8, 4 or 2");
-  const dim3 grid((unsigned)nsegs), block(kThreads);
+  const dim3 block(kThreads);
   const int sg = is_signed ? 1 : 0;
+  unsigned long long* dq = nullptr;
+  uint32_t dpar = 0;
+  // the queue consumer is a persistent grid (8 workgroups per CU)
+  const unsigned drain = (unsigned)std::min<uint64_t>(nsegs, 2048);
 
 #define ORCG_K(T, P, O, WKB, PIPE)                                                                   \
-  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN>), grid, block, 0, ctx->stream, d_src, \
-                     src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
-                     ctx->d_err)
-#define ORCG_KT(O, WKB, PIPE, MWV, DNV)                                              \
+  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF>), grid, block, 0, ctx->stream,   \
+                     d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
+                     ctx->d_err, dq, dpar)
+#define ORCG_KX(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                  \
   do {                                                                              \
     constexpr int MW = MWV;                                                         \
-    constexpr bool DN = DNV;                                                        \
+    constexpr int DN = (int)(DNV);                                                  \
+    constexpr int DF = DFV;                                                         \
+    const dim3 grid(GRIDV);                                                         \
     if (dst_bytes == 8) {                                                           \
       if (positions_mode) ORCG_K(int64_t, true, O, WKB, PIPE);                       \
       else ORCG_K(int64_t, false, O, WKB, PIPE);                                     \
@@ -1166,50 +1546,66 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
       else ORCG_K(int16_t, false, O, WKB, PIPE);                                     \
     }                                                                               \
   } while (0)
+#define ORCG_KT(O, WKB, PIPE, MWV, DNV) ORCG_KX(O, WKB, PIPE, MWV, DNV, 0, (unsigned)nsegs)
 
-  switch (ctx->rlev2_variant) {
+  // the default's instances
+  constexpr int kSer = kOptNTStore | kOptReuse | kOptFast | kOptT4;  // serial-walk paths
+  constexpr int kWide = kSer | kOptRegFill;
+  // a serial instance that queues short-run segments, then the dense
+  // instance that drains the queue
+#define ORCG_DEFERRING(O, WKB, MWV)                                                   \
+  do {                                                                              \
+    int rc_ = defer_queue(ctx, nsegs, &dq);                                          \
+    if (rc_) return rc_;                                                            \
+    dpar = (uint32_t)(ctx->defer_seq++ & 1u);                                       \
+    ORCG_KX(O, WKB, false, MWV, 0, 1, (unsigned)nsegs);                              \
+    ORCG_KX(kSer, 8, false, 6, 2, 2, drain);                                         \
+  } while (0)
+
+  int variant = ctx->rlev2_variant;
+  if (variant == 0) {
+    // By stream density: wide values (>= 5 stream bytes per value, e.g.
+    // W >= 40) stream best through 33 KB windows (4 WG/CU) filled through
+    // registers; narrower ones through 21 KB windows (6 WG/CU); both walk
+    // run headers with one wave and queue any segment whose first runs are
+    // short for the dense instance. Below 1.25 B/value the stream is likely
+    // made of short runs (low-cardinality columns: SHORT_REPEAT runs are
+    // 0.2-1 B/value): the dense instance runs it directly (parallel run
+    // discovery, 8.5 KB windows, 6 WG/CU) and falls back to the serial walk
+    // inside a segment whose runs are long. Measured: scripts/ab_rlev2.py,
+    // profiles/r02/sweep.md.
+    const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
+    variant = src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 4);
+  }
+  switch (variant) {
+    case 2: ORCG_DEFERRING(kWide, 33, 1); break;            // 33 KB register-filled serial + dense drain
+    case 3: ORCG_DEFERRING(kSer, 21, 6); break;             // 21 KB serial + dense drain
+    case 4: ORCG_KX(kSer, 8, false, 6, 2, 0, (unsigned)nsegs); break;   // dense v2, 8.5 KB
+    case 5: ORCG_KX(kSer, 12, false, 5, 2, 0, (unsigned)nsegs); break;  // dense v2, 12.5 KB
+#ifdef ORCG_AB_VARIANTS
     case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false); break;  // 21 KB + fast
     case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
-    case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 20, false, 4, true); break;  // dense-capable, 20.5 KB
-    case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 12, false, 5, true); break;  // dense-capable, 12.5 KB
+    case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 20, false, 4, true); break;  // dense v1, 20.5 KB
+    case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 12, false, 5, true); break;  // dense v1, 12.5 KB
     case 12: ORCG_KT(kOptNTStore | kOptFast, 21, true, 3, false); break;               // producer wave, 2 x 21 KB
     case 13: ORCG_KT(kOptNTStore | kOptFast, 13, true, 4, false); break;               // producer wave, 2 x 13 KB
-    case 14: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false); break;             // 9 + register fill
-    case 15: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 8, false, 6, true); break;    // dense-capable, 8.5 KB, 6 WG/CU
-    case 16: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 21, false, 6, false); break;  // 8 + T4
-    case 17: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptT4, 33, false, 1, false); break; // 14 + T4
-    case 18: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 12, false, 5, true); break;    // 11 + T4
-    case 19: ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 8, false, 6, true); break;     // 15 + T4
-    case 20: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptFast | kOptT4, 33, false, 1, false); break; // 17 + full-run fast paths
-    default: {
-      // ORCG_RLEV2_TILED picks the instance by stream density: wide values
-      // (>= 5 stream bytes per value, e.g. W >= 40) stream best through
-      // 33 KB windows (4 WG/CU) filled through registers (+2 % over
-      // LDS-DMA; the 21 KB instance cannot hold its loads without spilling
-      // at 6 WG/CU); narrower ones need more workgroups in
-      // flight per CU to keep HBM busy: 21 KB windows (6 WG/CU) + the
-      // predicate-free full-run path; below 1.25 bytes per value the stream
-      // may be made of short runs (low-cardinality columns: SHORT_REPEAT runs
-      // are 0.2-1 B/value), so an instance with the dense (parallel run
-      // discovery) mode runs: 5x faster on such streams. Its LDS (window +
-      // run table / DP table + stages / chain tables) sets the occupancy:
-      // 12.5 KB windows (5 WG/CU) from 0.75 B/value, 8.5 KB windows (6 WG/CU,
-      // +10 % on SHORT_REPEAT streams, -4..7 % on W=8 DIRECT / narrow DELTA
-      // from the extra window moves) below. Every instance walks
-      // DELTA headers through per-dword terminator nibbles (kOptT4: +5-7 % on
-      // DELTA streams, neutral elsewhere). Measured: scripts/ab_rlev2.py,
-      // profiles/r01/sweep.md; the 33 KB instance also carries the full-run
-      // fast paths (variant 20: +1 % W=64, +5 % W=32, +42 % DELTA, +18 % PATCHED
-      // over variant 17).
-      const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
-      if (src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptFast | kOptT4, 33, false, 1, false);
-      else if (4 * src_len >= 5 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 21, false, 6, false);
-      else if (4 * src_len >= 3 * est_values) ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 12, false, 5, true);
-      else ORCG_KT(kOptNTStore | kOptReuse | kOptFast | kOptT4, 8, false, 6, true);
-      break;
-    }
+    case 14: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false); break;  // 9 + register fill
+    case 15: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 8, false, 6, true); break;    // dense v1, 8.5 KB
+    case 16: ORCG_KT(kSer, 21, false, 6, false); break;                                // 21 KB serial, no queue
+    case 17: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptT4, 33, false, 1, false); break;  // 14 + T4
+    case 18: ORCG_KT(kSer, 12, false, 5, true); break;                                 // dense v1, 12.5 KB + T4
+    case 19: ORCG_KT(kSer, 8, false, 6, true); break;                                  // dense v1, 8.5 KB + T4
+    case 20: ORCG_KT(kWide, 33, false, 1, false); break;                               // 33 KB serial, no queue
+    case 21: ORCG_KT(kSer, 8, false, 6, 2); break;                                     // dense v2, 8.5 KB
+    case 22: ORCG_KT(kSer, 12, false, 5, 2); break;                                    // dense v2, 12.5 KB
+    case 23: ORCG_KT(kSer, 20, false, 4, 2); break;                                    // dense v2, 20.5 KB
+    case 24: ORCG_KT(kWide, 32, false, 1, 2); break;                                   // dense v2, 32.5 KB
+#endif
+    default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "unknown RLEv2 kernel variant");
   }
+#undef ORCG_DEFERRING
 #undef ORCG_KT
+#undef ORCG_KX
 #undef ORCG_K
   return hip_check(ctx, hipGetLastError(), "rlev2_tiled_kernel launch");
 }

@@ -8,6 +8,8 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the A/B build carries every tuning instance and the copy probes
+os.environ.setdefault("ORCG_LIB", "liborcgpu_ab.so")
 
 
 def main():

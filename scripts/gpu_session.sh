@@ -39,6 +39,32 @@ for s in $STEPS; do
       run cliff_sdir16 300 python scripts/ab_rlev2.py --data shortdirect --bits 16 --variants $V --rounds 3 --refs probe5 || true
       run cliff_sdir64 300 python scripts/ab_rlev2.py --data shortdirect --bits 64 --variants $V --rounds 3 --refs probe5 || true
       run cliff_smix32 300 python scripts/ab_rlev2.py --data shortmix --bits 32 --variants $V --rounds 3 --refs probe5 || true ;;
+    dense2)
+      V=${D2_VARIANTS:-19,21,22,23,24}
+      for spec in "repeat 12" "repeat 40" "repeat 64" "shortdirect 16" "shortdirect 64" "shortmix 32" "random 8" "delta 12" "random 64"; do
+        set -- $spec
+        run d2_$1_$2 300 python scripts/ab_rlev2.py --data $1 --bits $2 --variants $V --rounds 3 --refs copy || true
+      done ;;
+    phase)
+      V=${PH_VARIANTS:-19,21}
+      for spec in ${PH_SPECS:-"repeat:12" "shortdirect:16" "repeat:64"}; do
+        run ph_${spec/:/_} 300 env ORCG_LIB=liborcgpu_prof.so python scripts/phase_prof.py --data ${spec%%:*} --bits ${spec##*:} --variants $V || true
+      done ;;
+    sqpmc)
+      # SQ counters of one instance on one stream shape (separate passes)
+      export TMPDIR=/tmp
+      V=${SQ_VARIANT:-21}; D=${SQ_DATA:-repeat}; B=${SQ_BITS:-12}
+      i=0
+      for grp in "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_INSTS_VMEM_WR,SQ_INSTS_BRANCH,SQ_WAVE_CYCLES,SQ_BUSY_CYCLES" \
+                 "SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_SALU,SQ_ACTIVE_INST_LDS,SQ_WAIT_ANY,SQ_LDS_BANK_CONFLICT,SQ_ACTIVE_INST_ANY,SQ_INSTS_SMEM"; do
+        i=$((i+1))
+        run sqpmc_$i 120 rocprofv3 --kernel-trace --pmc ${grp//,/ } -d "$PWD/$OUT/sqpmc_$i" -o run --output-format csv -- python3 scripts/ab_rlev2.py --data $D --bits $B --variants $V --rounds 1 --iters 3 --refs "" || break
+      done ;;
+    sweep2)
+      V=${SW_VARIANTS:-0,2,3,4,5,16,20}
+      for spec in ${SW_SPECS:-"random:64" "random:48" "random:13" "random:8" "random:1" "delta:12" "patched:12" "repeat:12" "repeat:40" "repeat:64" "shortdirect:16" "shortdirect:64" "shortmix:32"}; do
+        run sw_${spec/:/_} 300 python scripts/ab_rlev2.py --data ${spec%%:*} --bits ${spec##*:} --variants $V --rounds 3 --refs copy,probe5 || true
+      done ;;
     benchwalk) run bench_walk 600 python bench.py --variant 1 --no-cpu-baseline ;;
     prof)
       export TMPDIR=/tmp

@@ -26,7 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=20_000_000)
     ap.add_argument("--bits", type=int, default=12)
-    ap.add_argument("--data", default="repeat", choices=["random", "delta", "repeat"])
+    ap.add_argument("--data", default="repeat")
     ap.add_argument("--variants", default="0")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--stride", type=int, default=10_000)
@@ -37,28 +37,11 @@ def main():
 
     L = orc_amd._lib.load()
     L.orcg_debug_phase_counters.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-    rng = np.random.default_rng(42)
-    n = args.rows
-    if args.data == "random":
-        v = rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=n, dtype=np.int64)
-        data, pos = orc_amd.encode_direct(v, True, aligned=True, rows_per_group=args.stride)
-    else:
-        if args.data == "repeat":
-            lens = rng.integers(3, 11, size=n // 6 + 16).astype(np.uint32)
-            lens = lens[: np.searchsorted(np.cumsum(lens), n)]
-            kinds = np.zeros(lens.size, dtype=np.uint8)
-            v = np.repeat(rng.integers(-(1 << (args.bits - 1)), 1 << (args.bits - 1), size=lens.size), lens)
-        else:
-            lens = np.full(n // 512, 512, dtype=np.uint32)
-            kinds = np.full(lens.size, 3, dtype=np.uint8)
-            v = np.cumsum(rng.integers(0, 1 << args.bits, size=n, dtype=np.int64)) + 1_000_000
-        n = int(lens.sum())
-        v = v[:n].astype(np.int64)
-        data, offs = orc_amd.encode_runs(v, True, kinds, lens)
-        starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
-        g = np.arange(0, n, args.stride)
-        ri = np.searchsorted(starts, g, side="right") - 1
-        pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from streams import make
+
+    v, data, pos = make(args.data, args.bits, args.rows, args.stride)
+    n = int(v.size)
     stream = torch.cuda.Stream()
     ctx = orc_amd.Context(0, stream=stream)
     with torch.cuda.stream(stream):

@@ -311,7 +311,7 @@ def test_patched_full_runs_patch_layouts(layout):
         ri = np.searchsorted(starts, g, side="right") - 1
         pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
         d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
-        for variant in (0, 8, 9, 10, 11, 15, 16, 17, 18, 19, 20):
+        for variant in orc_amd.rlev2_variants():
             ctx.set_rlev2_variant(variant)
             out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
             orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, True, out)
@@ -319,4 +319,98 @@ def test_patched_full_runs_patch_layouts(layout):
             got = out.cpu().numpy()
             assert np.array_equal(got, want), "variant %d stride %d: first mismatch at %d" % (
                 variant, stride, int(np.argmax(got != want)))
+    ctx.set_rlev2_variant(0)
+
+
+def _mixed_segments(orc, rng, nseg, stride):
+    """Row groups alternating between long DIRECT runs of 64-bit values and
+    short SHORT_REPEAT / short DIRECT runs of wide values: overall >= 1.25
+    stream bytes per value (the default picks a serial-walk instance), with
+    every other segment made of short runs (queued for the dense instance)."""
+    vals, kinds, lens = [], [], []
+    for s in range(nseg):
+        left = stride
+        if s % 2 == 0:
+            while left:
+                L = min(512, left)
+                vals.append(rng.integers(-(1 << 62), 1 << 62, size=L))
+                kinds.append(1)
+                lens.append(L)
+                left -= L
+        else:
+            while left:
+                if rng.random() < 0.5 and left >= 3:
+                    L = int(min(rng.integers(3, 11), left))
+                    vals.append(np.full(L, int(rng.integers(-(1 << 50), 1 << 50))))
+                    kinds.append(0)
+                else:
+                    L = int(min(rng.integers(1, 9), left))
+                    vals.append(rng.integers(-(1 << 40), 1 << 40, size=L))
+                    kinds.append(1)
+                lens.append(L)
+                left -= L
+    v = np.concatenate(vals).astype(np.int64)
+    lens = np.array(lens, dtype=np.uint32)
+    data, offs = orc.encode_runs(v, True, np.array(kinds, np.uint8), lens)
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    g = np.arange(0, v.size, stride)
+    ri = np.searchsorted(starts, g, side="right") - 1
+    pos = np.stack([offs[ri].astype(np.uint64), (g - starts[ri]).astype(np.uint64)], axis=1)
+    return v, data, pos
+
+
+def test_short_run_segments_are_queued_for_the_dense_instance():
+    """The serial-walk instances queue short-run segments and the dense
+    instance drains the queue in the same decode: bit-exact against the
+    oracle for every instance the default launches, for value sub-ranges,
+    and across repeated launches (the queue resets itself)."""
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(21)
+    ctx = orc_amd.default_context(0)
+    stride = 5000
+    v, data, pos = _mixed_segments(orc_amd, rng, 40, stride)
+    want = oracle.rlev2_decode(data.tobytes(), v.size, True)
+    np.testing.assert_array_equal(want, v)
+    assert data.size >= 1.25 * v.size
+    d_src = torch.from_numpy(data).cuda()
+    d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+    for variant in orc_amd.rlev2_variants():
+        ctx.set_rlev2_variant(variant)
+        for _ in range(3):
+            out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, True, out)
+            ctx.synchronize()
+            got = out.cpu().numpy()
+            assert np.array_equal(got, want), "variant %d: first mismatch at %d" % (variant, int(np.argmax(got != want)))
+        for a, b in [(7_001, 7_002), (4_999, 15_001), (100_000, 200_000 - 3)]:
+            o2 = torch.zeros(b - a, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, b - a, True, o2, value_begin=a)
+            ctx.synchronize()
+            np.testing.assert_array_equal(o2.cpu().numpy(), want[a:b])
+    ctx.set_rlev2_variant(0)
+
+
+def test_queued_segment_reports_truncation():
+    """A short-run segment that runs into a truncated run: the dense instance
+    draining the queue reports the reference's error at the first missing
+    value, like the serial walk."""
+    import orc_amd
+
+    rng = np.random.default_rng(3)
+    v = np.repeat(rng.integers(-(1 << 60), 1 << 60, size=3000), 5)
+    data, _ = orc_amd.encode_runs(v, True, np.zeros(3000, np.uint8), np.full(3000, 5, np.uint32))
+    bad = data.tobytes() + bytes([0x5E, 0x03, 0x5C])  # a DIRECT header whose data is missing
+    with pytest.raises(oracle.OracleError) as want:
+        oracle.RleDecoderV2(bad, True).next(v.size + 1)
+    ctx = orc_amd.default_context(0)
+    for variant in orc_amd.rlev2_variants():
+        if variant == 1:
+            continue
+        ctx.set_rlev2_variant(variant)
+        with pytest.raises(orc_amd.ParseError) as got:
+            orc_amd.rlev2_decode(bad, v.size + 1, True)
+        assert str(got.value) == str(want.value), variant
     ctx.set_rlev2_variant(0)
