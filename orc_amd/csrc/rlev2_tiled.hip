@@ -417,8 +417,13 @@ __device__ __forceinline__ void fill(uint32_t* win, __amdgpu_buffer_rsrc_t rs, u
 }
 
 struct WalkResult {
-  uint32_t n, stop, dpos, dval;
+  uint32_t n, stop, dpos, dval, items;
 };
+
+// Work items of a serial pass (the walk publishes item ends): a group of up
+// to 64 consecutive short runs, expanded one lane per run, or one long /
+// PATCHED_BASE run (flag kItemLong), expanded by a whole wave.
+constexpr uint16_t kItemLong = 0x8000;
 
 // The serial walk's view of a run: bytes, values and the error parse_run
 // would report, in its order. SHORT_REPEAT / DIRECT from the first two
@@ -426,13 +431,18 @@ struct WalkResult {
 // (two varints of <= 11 bytes: every writer's); PATCHED_BASE and longer
 // varints through parse_run.
 template <bool kT4>
-__device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint64_t avail, int is_signed,
-                                            uint32_t* bytes, uint32_t* L, uint32_t* err) {
+__device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint32_t avail, int is_signed,
+                                            uint32_t* bytes, uint32_t* L, uint32_t* err, uint32_t* rkind) {
   const uint32_t fb = hw.byte(lp), kind = fb >> 6;
   *err = kErrNone;
-  if (kind == 0) {
-    *bytes = 2u + ((fb >> 3) & 7u);
-    *L = (fb & 7u) + 3u;
+  *rkind = kind;
+  if (kind < 2) {
+    // SHORT_REPEAT / DIRECT, straight-line scalar code (a DIRECT run short
+    // of its second header byte has >= 2 bytes > avail: the same bad read)
+    const uint32_t L2 = ((fb & 1u) << 8 | hw.byte(lp + 1)) + 1u;
+    const uint32_t db = 2u + (fbs_width((fb >> 1) & 0x1fu) * L2 + 7u) / 8u;
+    *bytes = kind ? db : 2u + ((fb >> 3) & 7u);
+    *L = kind ? L2 : (fb & 7u) + 3u;
     if (*bytes > avail) *err = kErrBadRead;
     return;
   }
@@ -445,12 +455,6 @@ __device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint
     }
     const uint32_t L2 = ((fb & 1u) << 8 | hw.byte(lp + 1)) + 1u;
     const uint32_t code = (fb >> 1) & 0x1fu;
-    if (kind == 1) {
-      *L = L2;
-      *bytes = 2u + (fbs_width(code) * L2 + 7u) / 8u;
-      if (*bytes > avail) *err = kErrBadRead;
-      return;
-    }
     // DELTA: varint lengths from the terminator mask of bytes lp+2 .. lp+25
     // (the slice's per-dword terminator nibbles, gathered and realigned)
     const uint32_t o = lp + 2u - hw.base, i0 = o >> 2, sh = o & 3u;
@@ -495,41 +499,179 @@ __device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint
 
 // Wave-uniform header walk over the window [wpos, wpos + kWin): records runs
 // starting at pos.. into (run_off, run_val) until the next run starts past
-// kWin - kMaxRun, leaves the segment, or the table is full.
+// kWin - kMaxRun, leaves the segment, or the table is full. With `pub` the
+// walk also cuts the runs into work items (`items`, ends by run index) and
+// publishes the item count as items close, so expanding waves start early.
 template <uint32_t kWin, uint32_t kCap, bool kT4 = false, typename OffT = uint32_t>
 __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, uint32_t* run_val,
                                            uint64_t wpos, uint64_t pos, uint64_t vi, uint64_t seg_end,
                                            uint64_t src_len, uint64_t value_end, int is_signed,
                                            unsigned long long* err, int lane, uint32_t lim = kWin,
-                                           uint32_t cap = kCap, uint32_t* pub = nullptr) {
+                                           uint32_t cap = kCap, uint32_t* pub = nullptr,
+                                           uint16_t* items = nullptr) {
+  static_assert(kCap < kItemLong, "run indices must leave the item flag free");
   constexpr uint32_t kChunk = kWin - kMaxRun;
-  uint64_t p = pos, v = vi;
+  // everything wave-uniform and 32-bit, relative to the window / the first
+  // value: the loop stays on the scalar unit (no 64-bit VALU compares)
+  const uint32_t sp = (uint32_t)(pos - wpos);
+  const uint32_t a_seg = seg_end - wpos < 0xfffff000ull ? (uint32_t)(seg_end - wpos) : 0xfffff000u;
+  const uint32_t a_src = src_len - wpos < 0xfffff000ull ? (uint32_t)(src_len - wpos) : 0xfffff000u;
+  const uint32_t v_lim = value_end - vi < 0xffffffffull ? (uint32_t)(value_end - vi) : 0xffffffffu;
+  uint32_t lp = sp, vr = 0;
   uint32_t n = 0, stop = 0;
   LaneWin hw;
-  while (p < seg_end && v < value_end && n < cap) {
-    const uint32_t lp = (uint32_t)(p - wpos);
+  hw.load(win, sp, kWin / 4 + 8, lane);
+  // run k waits in lane k % 64 (r_off, r_val) until the table write of its
+  // batch: one LDS round trip (and one release store) per item or per 64
+  // runs instead of one per run
+  uint32_t r_off = 0, r_val = 0, flushed = 0, gstart = 0, nitems = 0;
+  auto flush = [&]() {
+    const uint32_t r = flushed + (((uint32_t)lane - flushed) & (kWave - 1));
+    if (r < n) {
+      run_off[r] = (OffT)r_off;
+      run_val[r] = r_val;
+    }
+    flushed = n;
+  };
+  const uint32_t lim_all = uni(min(min(a_src, a_seg), lim));
+  const bool items_on = uni(pub != nullptr ? 1u : 0u) != 0;
+  while (lp < a_seg && vr < v_lim && n < cap) {
     if (lp >= kChunk && n > 0) break;  // starts in the next window
-    hw.cover(win, lp, kWin / 4 + 8, lane);
-    uint32_t rbytes, rL, e;
-    walk_extent<kT4>(hw, lp, src_len - p, is_signed, &rbytes, &rL, &e);
-    if (e == kErrNone && p + rbytes > seg_end) e = kErrBadSegment;
-    if (e == kErrNone && lp + rbytes > lim) e = kErrBadRead;  // only a corrupt varint gets here
-    if (e != kErrNone) {
-      if (lane == 0) report(err, v, e);
+    if (lp + kHdrLim > hw.base + 256) hw.load(win, lp, kWin / 4 + 8, lane);
+    // the two header bytes from two lanes of the slice, realigned on the
+    // scalar unit; SHORT_REPEAT / DIRECT sized inline (branch-free selects),
+    // DELTA / PATCHED_BASE through walk_extent
+    const uint32_t o = lp - hw.base, wi = o >> 2;
+    const uint64_t w2 = ((uint64_t)rdlane(hw.word, wi + 1) << 32) | rdlane(hw.word, wi);
+    const uint32_t hdr = (uint32_t)(w2 >> ((o & 3u) * 8u));
+    const uint32_t fb = hdr & 0xffu, kind = fb >> 6;
+    uint32_t rbytes, rL, e = kErrNone;
+    if (kind < 2) {
+      const uint32_t L2 = ((fb & 1u) << 8 | ((hdr >> 8) & 0xffu)) + 1u;
+      const uint32_t code = (fb >> 1) & 0x1fu;
+      const uint32_t wt = (uint32_t)(0x40383028201E1C1Aull >> (((code - 24u) & 7u) * 8u)) & 0xffu;
+      const uint32_t W = code < 24 ? code + 1u : wt;  // fbs_width
+      uint32_t bits;
+      asm("s_mul_i32 %0, %1, %2" : "=s"(bits) : "s"(W), "s"(L2));
+      rbytes = kind ? 2u + ((bits + 7u) >> 3) : 2u + ((fb >> 3) & 7u);
+      rL = kind ? L2 : (fb & 7u) + 3u;
+    } else {
+      uint32_t kd;
+      walk_extent<kT4>(hw, lp, a_src - lp, is_signed, &rbytes, &rL, &e, &kd);
+      rbytes = uni(rbytes);  // keep the merged values scalar
+      rL = uni(rL);
+      e = uni(e);
+    }
+    if (e != kErrNone || lp + rbytes > lim_all) {
+      // the first failing check, in the order parse / segment / window
+      if (e == kErrNone)
+        e = lp + rbytes > a_src ? kErrBadRead : (lp + rbytes > a_seg ? kErrBadSegment : kErrBadRead);
+      if (lane == 0) report(err, vi + vr, e);
       stop = 1;
       break;
     }
-    if (lane == 0) {
-      run_off[n] = (OffT)lp;
-      run_val[n] = (uint32_t)(v - vi);
-      // expanding waves may claim the run as soon as it is published
-      if (pub) __hip_atomic_store(pub, n + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    const uint32_t slot = n & (kWave - 1);
+    // (the lane select goes through m0: one scalar operand per VALU op)
+    asm volatile("s_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+                 : "+v"(r_off), "+v"(r_val)
+                 : "s"(uni(lp)), "s"(uni(vr)), "s"(uni(slot))
+                 : "m0");
     ++n;
-    p += rbytes;
-    v += rL;
+    lp += rbytes;
+    vr += rL;
+    if (items_on) {
+      if (rL > kShortL || kind == 2) {
+        // close the open group of short runs, then this run as its own item
+        flush();
+        const uint32_t grp = n - 1 > gstart ? 1u : 0u;
+        if (lane == 0) {
+          if (grp) items[nitems] = (uint16_t)(n - 1);
+          items[nitems + grp] = (uint16_t)(n | kItemLong);
+        }
+        nitems += grp + 1;
+        gstart = n;
+        // expanding waves may claim the items as soon as they are published
+        if (lane == 0) __hip_atomic_store(pub, nitems, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if (n - gstart == kWave) {
+        flush();
+        if (lane == 0) items[nitems] = (uint16_t)n;
+        ++nitems;
+        gstart = n;
+        if (lane == 0) __hip_atomic_store(pub, nitems, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else if (n - flushed == kWave) {
+      flush();
+    }
   }
-  return WalkResult{n, stop, (uint32_t)(p - pos), (uint32_t)(v - vi)};
+  if (n != flushed) flush();
+  if (pub && n > gstart) {
+    // the last group: published by the caller's final (walk done) store
+    if (lane == 0) items[nitems] = (uint16_t)n;
+    ++nitems;
+  }
+  return WalkResult{n, stop, lp - sp, vr, nitems};
+}
+
+// Value j of a short run (kind SHORT_REPEAT / DIRECT / DELTA) parsed at
+// window offset `hoff`; `acc` carries a variable-width DELTA run's |delta| sum.
+__device__ __forceinline__ uint64_t short_value(const uint32_t* win, const Run& r, uint32_t hoff, uint32_t j,
+                                                int is_signed, uint64_t& acc) {
+  if (r.kind == 0) return r.a;
+  if (r.kind == 1) {
+    const uint32_t bit = j * r.W;
+    const uint32_t br = hoff + r.data + (bit >> 3);
+    uint64_t v = field(lds12(win, br), br, bit & 7u, r.W);
+    return is_signed ? unzigzag(v) : v;
+  }
+  if (r.W == 0) return r.a + (uint64_t)j * r.b;
+  if (j == 0) return r.a;
+  const uint64_t v1 = r.a + r.b;
+  if (j == 1) return v1;
+  const uint32_t bit = (j - 2) * r.W;
+  const uint32_t br = hoff + r.data + (bit >> 3);
+  acc += field(lds12(win, br), br, bit & 7u, r.W);
+  return (int64_t)r.b < 0 ? v1 - acc : v1 + acc;
+}
+
+// Expand runs [r0, r1) (r1 - r0 <= 64, each SHORT_REPEAT / DIRECT / DELTA of
+// <= kShortL values) one lane per run, storing straight to the output.
+template <int kOpt, typename T, typename OffT>
+__device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_off, const uint32_t* s_val,
+                                             uint32_t r0, uint32_t r1, uint64_t vi, int is_signed,
+                                             uint64_t value_begin, uint64_t value_end, T* dst, int lane) {
+  const uint32_t r = r0 + (uint32_t)lane;
+  const bool act = r < r1;
+  const uint32_t hoff = act ? s_off[r] : s_off[r0];
+  const uint64_t o0 = vi + (act ? s_val[r] : 0u);
+  const uint32_t w0 = hoff >> 2, sh = hoff & 3u;
+  const uint32_t d0 = win[w0], d1 = win[w0 + 1], d2 = win[w0 + 2], d3 = win[w0 + 3];
+  const uint32_t b0 = __builtin_amdgcn_alignbyte(d1, d0, sh), b1 = __builtin_amdgcn_alignbyte(d2, d1, sh),
+                 b2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+  const uint32_t fb = b0 & 0xffu;
+  if (__ballot(act && (fb >> 6) != 0) == 0) {
+    // SHORT_REPEAT only: W + 1 value bytes, big endian
+    const uint32_t L = act ? (fb & 7u) + 3u : 0u;
+    const uint32_t nb = ((fb >> 3) & 7u) + 1u;
+    const uint64_t be = ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(b1, b0, 1)) << 32) |
+                        __builtin_bswap32(__builtin_amdgcn_alignbyte(b2, b1, 1));
+    uint64_t a = be >> (64 - 8 * nb);
+    if (is_signed) a = unzigzag(a);
+    for (uint32_t j = 0; __ballot(j < L) != 0; ++j) {
+      const uint64_t o = o0 + j;
+      if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), a);
+    }
+    return;
+  }
+  const Run run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
+  const uint32_t L = act ? run.L : 0u;
+  uint64_t acc = 0;
+  for (uint32_t j = 0; __ballot(j < L) != 0; ++j) {
+    const uint64_t o = o0 + j;
+    if (j < L) {
+      const uint64_t x = short_value(win, run, hoff, j, is_signed, acc);
+      if (o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), x);
+    }
+  }
 }
 
 // ---- dense mode -----------------------------------------------------------
@@ -1007,27 +1149,6 @@ __device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT
   return DenseResult{uni(total), uni(s_ctl[3]), uni(s_ctl[1]), uni(s_ctl[2])};
 }
 
-// Value j of a short run (kind SHORT_REPEAT / DIRECT / DELTA) parsed at
-// window offset `hoff`; `acc` carries a variable-width DELTA run's |delta| sum.
-__device__ __forceinline__ uint64_t short_value(const uint32_t* win, const Run& r, uint32_t hoff, uint32_t j,
-                                                int is_signed, uint64_t& acc) {
-  if (r.kind == 0) return r.a;
-  if (r.kind == 1) {
-    const uint32_t bit = j * r.W;
-    const uint32_t br = hoff + r.data + (bit >> 3);
-    uint64_t v = field(lds12(win, br), br, bit & 7u, r.W);
-    return is_signed ? unzigzag(v) : v;
-  }
-  if (r.W == 0) return r.a + (uint64_t)j * r.b;
-  if (j == 0) return r.a;
-  const uint64_t v1 = r.a + r.b;
-  if (j == 1) return v1;
-  const uint32_t bit = (j - 2) * r.W;
-  const uint32_t br = hoff + r.data + (bit >> 3);
-  acc += field(lds12(win, br), br, bit & 7u, r.W);
-  return (int64_t)r.b < 0 ? v1 - acc : v1 + acc;
-}
-
 // Expand runs [r0, r1) of the run table with one wave: maximal groups of
 // consecutive short runs (<= kStage values) are decoded one lane per run into
 // the wave's LDS stage and flushed with coalesced stores; any other run
@@ -1126,6 +1247,7 @@ struct Dense2Lds {
     struct {
       uint16_t off[kDenseRuns];
       uint32_t val[kDenseRuns];
+      uint16_t items[kDenseRuns];  // serial passes: work item ends
     } tab;
     uint16_t nxt[2 * kSlab];
   };
@@ -1180,8 +1302,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   uint16_t* s_nxt2 = nullptr;   // v2: successor table, marks, stages
   uint32_t* s_mark2 = nullptr;
   uint64_t* s_stage2 = nullptr;
+  uint16_t* s_items = nullptr;  // serial passes (non-pipelined): work item ends
   if constexpr (kDense == 2) {
     __shared__ __attribute__((aligned(16))) Dense2Lds s_d2;
+    s_items = s_d2.tab.items;
     s_off[0] = s_d2.tab.off;
     s_val[0] = s_d2.tab.val;
     s_nxt2 = s_d2.nxt;
@@ -1194,6 +1318,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       s_val[b] = s_tab[b] + kCap;
     }
     s_tab0 = s_tab[0];
+    if constexpr (!kPipe) {
+      __shared__ uint16_t s_itm[kCap];
+      s_items = s_itm;
+    }
   }
 
   const int tid = (int)threadIdx.x;
@@ -1329,9 +1457,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
                                value_begin, value_end, dst, lane);
           }
         } else {
-          // Wave 0 walks and publishes each run as it is found; every wave
-          // (wave 0 once its walk is done) claims published runs from an LDS
-          // counter and expands them, so the walk overlaps the expansion.
+          // Wave 0 walks and publishes work items (a group of short runs or
+          // one long run) as they close; every wave (wave 0 once its walk is
+          // done) claims published items from an LDS counter and expands
+          // them, so the walk overlaps the expansion.
           uint32_t* s_pub = &s_sync[sync_par][0];
           uint32_t* s_claim = &s_sync[sync_par][1];
           if (wave == 0) {
@@ -1344,13 +1473,13 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             const uint32_t cap = ((kDense || kDefer == 1) && probe) ? (kDense == 2 ? 4u : (kDefer == 1 ? 8u : 32u)) : kCap;
             const WalkResult w = walk<kWin, kCap, (kOpt & kOptT4) != 0, OffT>(s_win[0], s_off[0], s_val[0], wpos, pos, vi,
                                                                     seg_end, src_len, value_end, is_signed, err,
-                                                                    lane, need, cap, s_pub);
+                                                                    lane, need, cap, s_pub, s_items);
             if (lane == 0) {
               s_ctl[0][0] = w.n;
               s_ctl[0][1] = w.stop;
               s_ctl[0][2] = w.dpos;
               s_ctl[0][3] = w.dval;
-              __hip_atomic_store(s_pub, w.n | kWalkDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_store(s_pub, w.items | kWalkDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             __builtin_amdgcn_s_setprio(0);
           }
@@ -1364,9 +1493,15 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               if (k < (pub & ~kWalkDone) || (pub & kWalkDone)) break;
               __builtin_amdgcn_s_sleep(1);
             }
-            if (k >= (pub & ~kWalkDone)) break;  // the walk is done and every run is claimed
-            expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][k]), vi + uni(s_val[0][k]), is_signed,
-                             value_begin, value_end, dst, lane);
+            if (k >= (pub & ~kWalkDone)) break;  // the walk is done and every item is claimed
+            const uint32_t e = uni(s_items[k]);
+            const uint32_t r0 = k ? (uni(s_items[k - 1]) & ~(uint32_t)kItemLong) : 0u;
+            if (e & kItemLong)
+              expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][r0]), vi + uni(s_val[0][r0]), is_signed,
+                               value_begin, value_end, dst, lane);
+            else
+              group_expand<kOpt>(s_win[0], s_off[0], s_val[0], r0, e, vi, is_signed, value_begin, value_end, dst,
+                                 lane);
           }
           // the other parity's counters are idle: clear them for the next serial pass
           if (tid == 0) {
