@@ -190,6 +190,12 @@ int orcg_reader_last_timings(const orcg_reader* r, double* out5);
  * (ColumnReader::seekToRowGroup's PositionProvider, no host work) [0] and by
  * a host header walk (files without a row index) [1]. */
 int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2);
+/* RLEv2 streams of the last read decoded by a stripe's multi-stream launches
+ * (every stream whose value count is known on the host: one launch per
+ * kernel instance per stripe instead of one per stream). */
+uint64_t orcg_reader_last_batched_streams(const orcg_reader* r);
+/* Multi-stream batching on (default) / off (one launch per stream; A/B). */
+int orcg_reader_set_stream_batching(orcg_reader* r, int on);
 
 #ifdef __cplusplus
 }

@@ -164,6 +164,8 @@ SIGNATURES += [
     ("orcg_reader_metadata_key", [vp, u32], cp),
     ("orcg_reader_metadata_value", [vp, u32, ctypes.POINTER(u64)], vp),
     ("orcg_reader_set_lazy_dictionary", [vp, i32], i32),
+    ("orcg_reader_last_batched_streams", [vp], u64),
+    ("orcg_reader_set_stream_batching", [vp, i32], i32),
     ("orcg_reader_is_selected", [vp, u32], i32),
     ("orcg_row_reader_create", [vp, ctypes.POINTER(RowReaderOptions), ctypes.POINTER(vp)], i32),
     ("orcg_row_reader_destroy", [vp], None),

@@ -51,6 +51,27 @@ struct Ctx {
   void* d_defer = nullptr;  // RLEv2 short-run segment queue (rlev2_tiled.hip defer_queue)
   uint64_t defer_cap = 0;
   uint64_t defer_seq = 0;  // launches that used the queue (count parity)
+  int num_cus = 0;         // compute units of `device` (0 = not queried yet)
+  // job tables of multi-stream RLEv2 launches: a pinned host ring and its
+  // device mirror (launch_rlev2_multi)
+  void* h_jobs = nullptr;
+  void* d_jobs = nullptr;
+  uint64_t jobs_cap = 0, jobs_used = 0;
+};
+
+// One RLEv2 stream of a multi-stream launch: its bytes, segment table
+// ({byte offset, value index} per segment), output (int64) and value count;
+// seg_base = the launch-wide index of its first segment (set by the launcher).
+struct RleJob {
+  const uint8_t* src;
+  uint64_t src_len;
+  const uint64_t* segtab;
+  uint64_t nsegs;
+  void* dst;
+  uint64_t nvalues;
+  uint64_t seg_base;
+  uint32_t is_signed;
+  uint32_t pad;
 };
 
 int set_error(Ctx* ctx, int status, const std::string& msg);
@@ -74,6 +95,11 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
                        void* d_dst, int dst_bytes);
+
+// Every stream of `jobs` (segment-table mode, int64 output) in one launch per
+// instance the default's density rule picks (or the pinned variant);
+// variant 1 falls back to one launch per stream.
+int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs);
 
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
                    bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst);

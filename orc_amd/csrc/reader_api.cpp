@@ -266,6 +266,7 @@ struct orcg_reader {
   DevSlot* D = nullptr;
   double timings[5] = {0, 0, 0, 0, 0};
   uint64_t stream_stats[2] = {0, 0};  // last read: RLE streams cut by the row index, by host plans
+  uint64_t batched_streams = 0;       // last read: RLEv2 streams decoded by multi-stream launches
 
   // Checks whose operands are device scalars (dictionary blob size, varint
   // counts, string bytes): their D2H copies are queued on the stream and the
@@ -307,7 +308,19 @@ struct orcg_reader {
   int segments(Col& c, int slot, bool boolean, const uint64_t** d_seg, uint64_t* nseg);
   // RLE integer stream: v1 for DIRECT / DICTIONARY encodings (convertRleVersion,
   // DictionaryLoader.hh:42) unless force_v2 (Decimal64ColumnReaderV2 is always RLEv2)
-  int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out, bool force_v2 = false);
+  // (*out: the stream's values, decoded by this stripe's multi-stream batch
+  // when collect() queued it, else allocated and decoded now)
+  int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** out, bool force_v2 = false);
+  // Multi-stream batch: before decode(), the RLEv2 streams whose value
+  // counts and segments are known without device results (columns with no
+  // PRESENT stream, under parents with none) are queued and decoded by one
+  // launch per kernel instance (launch_rlev2_multi); decode() then finds
+  // their outputs here.
+  bool batch_on = true;
+  std::vector<RleJob> batch;
+  std::unordered_map<uint64_t, std::pair<int64_t*, uint64_t>> batched;  // (column, slot) -> (values, count)
+  int queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2);
+  int collect(uint32_t id, uint64_t n, const int64_t* rg_rows);
   int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out);
   int nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out);
   int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
@@ -414,7 +427,16 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
   return ORCG_OK;
 }
 
-int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t* out, bool force_v2) {
+int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** pout, bool force_v2) {
+  const uint64_t key = (uint64_t)(&c - H->cols.data()) * 8 + (uint64_t)slot;
+  const auto it = batched.find(key);
+  if (it != batched.end() && it->second.second == count) {
+    *pout = it->second.first;
+    return ORCG_OK;
+  }
+  int64_t* out = alloc<int64_t>(count);
+  if (!out) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  *pout = out;
   StreamBuf& sb = c.s[slot];
   if (count == 0) return ORCG_OK;
   if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
@@ -434,6 +456,69 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   else
     rc = launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
   return rc ? fail_ctx(rc) : ORCG_OK;
+}
+
+int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2) {
+  Col& c = H->cols[id];
+  StreamBuf& sb = c.s[slot];
+  // left to decode(): empty or missing streams, RLEv1, a host plan short of
+  // values (decode() raises the error in column order)
+  if (count == 0 || !sb.present) return ORCG_OK;
+  if (!force_v2 && (c.encoding == kDirect || c.encoding == kDictionary)) return ORCG_OK;
+  if (!sb.pos && count > sb.plan->values) return ORCG_OK;
+  const uint64_t* d_seg;
+  uint64_t nseg;
+  int rc = segments(c, slot, false, &d_seg, &nseg);
+  if (rc) return rc;
+  int64_t* out = alloc<int64_t>(count);
+  if (!out) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  RleJob j{};
+  j.src = D->d_stage + sb.host_off;
+  j.src_len = sb.len;
+  j.segtab = d_seg;
+  j.nsegs = nseg;
+  j.dst = out;
+  j.nvalues = count;
+  j.is_signed = is_signed ? 1u : 0u;
+  batch.push_back(j);
+  batched[(uint64_t)id * 8 + (uint64_t)slot] = {out, count};
+  return ORCG_OK;
+}
+
+// The streams decode() will read with host-known counts, in its order
+// (same slots, signedness and counts as decode()'s int_stream calls).
+int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
+  Col& c = H->cols[id];
+  if (!selected[id] || !c.supported) return ORCG_OK;
+  if (c.s[kSlotPresent].present) return ORCG_OK;  // its counts come from the device
+  cur_rows = rg_rows;
+  cur_n = n;
+  cur_in_nn = nullptr;
+  cur_row_nn = nullptr;
+  const uint32_t k = c.kind;
+  int rc = ORCG_OK;
+  if (k == ORCG_TYPE_DECIMAL) {
+    if (decimal_as_long && footer.types[id].precision <= 18) rc = queue_stream(id, kSlotData, true, n, true);
+    else rc = queue_stream(id, kSlotSecondary, true, n, false);
+  } else if (k == ORCG_TYPE_TIMESTAMP || k == ORCG_TYPE_TIMESTAMP_INSTANT) {
+    rc = queue_stream(id, kSlotData, true, n, false);
+    if (!rc) rc = queue_stream(id, kSlotSecondary, false, n, false);
+  } else if (is_int_kind(k)) {
+    rc = queue_stream(id, kSlotData, true, n, false);
+  } else if (is_string_kind(k)) {
+    if (c.encoding == kDictionary || c.encoding == kDictionaryV2) {
+      rc = queue_stream(id, kSlotLength, false, c.dict_size, false);
+      if (!rc) rc = queue_stream(id, kSlotData, false, n, false);
+    } else {
+      rc = queue_stream(id, kSlotLength, false, n, false);
+    }
+  } else if (k == ORCG_TYPE_LIST || k == ORCG_TYPE_MAP) {
+    rc = queue_stream(id, kSlotLength, false, n, false);
+  } else if (k == ORCG_TYPE_STRUCT) {
+    for (uint32_t st : footer.types[id].subtypes)
+      if ((rc = collect(st, n, rg_rows))) break;
+  }
+  return rc;
 }
 
 int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out) {
@@ -504,8 +589,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (decimal_as_long && t.precision <= 18) {
       // Decimal64ColumnReaderV2 (ColumnReader.cc:1529-1576): RLEv2 unscaled values
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64V2 column. ColumnId=" + cid);
-      ORCG_ALLOC(int64_t, dense, nonnull);
-      if ((rc = int_stream(c, kSlotData, true, nonnull, dense, true))) return rc;
+      int64_t* dense;
+      if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, true))) return rc;
       if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
     } else {
       // Decimal64ColumnReader / Decimal128ColumnReader (:1384-1527): varint
@@ -513,8 +598,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64Column");
       if (!has_sec) return fail(ORCG_PARSE_ERROR, "SECONDARY stream not found in Decimal64Column");
       const bool wide = t.precision > 18;
-      ORCG_ALLOC(int64_t, scales, nonnull);
-      if ((rc = int_stream(c, kSlotSecondary, true, nonnull, scales))) return rc;
+      int64_t* scales;
+      if ((rc = int_stream(c, kSlotSecondary, true, nonnull, &scales))) return rc;
       const StreamBuf& sb = c.s[kSlotData];
       const uint8_t* d_src = D->d_stage + sb.host_off;
       uint64_t ntiles = 0;
@@ -544,16 +629,15 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     // TimestampColumnReader (:259-349): seconds (signed RLE), nanos (unsigned RLE)
     if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Timestamp column");
     if (!has_sec) return fail(ORCG_PARSE_ERROR, "SECONDARY stream not found in Timestamp column");
-    ORCG_ALLOC(int64_t, secs, nonnull);
-    ORCG_ALLOC(int64_t, nanos, nonnull);
-    if ((rc = int_stream(c, kSlotData, true, nonnull, secs))) return rc;
-    if ((rc = int_stream(c, kSlotSecondary, false, nonnull, nanos))) return rc;
+    int64_t *secs, *nanos;
+    if ((rc = int_stream(c, kSlotData, true, nonnull, &secs))) return rc;
+    if ((rc = int_stream(c, kSlotSecondary, false, nonnull, &nanos))) return rc;
     if ((rc = launch_timestamp(ctx, secs, nanos, nonnull, kOrcEpochUtc))) return fail_ctx(rc);
     if (!(c.data = place_i64(secs)) || !(c.secondary = place_i64(nanos))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (is_int_kind(k)) {
     if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Integer column");
-    ORCG_ALLOC(int64_t, dense, nonnull);
-    if ((rc = int_stream(c, kSlotData, true, nonnull, dense))) return rc;
+    int64_t* dense;
+    if ((rc = int_stream(c, kSlotData, true, nonnull, &dense))) return rc;
     if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (k == ORCG_TYPE_BOOLEAN || k == ORCG_TYPE_BYTE) {
     if (!has_data)
@@ -599,9 +683,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       const std::string cid = std::to_string(id);
       if (dict_size > 0 && !has_len)
         return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDictionaryColumn for column " + cid);
-      ORCG_ALLOC(int64_t, dlen, dict_size);
+      int64_t* dlen;
       ORCG_ALLOC(int64_t, doff, dict_size + 1);
-      if ((rc = int_stream(c, kSlotLength, false, dict_size, dlen))) return rc;
+      if ((rc = int_stream(c, kSlotLength, false, dict_size, &dlen))) return rc;
       if ((rc = launch_flag_negative(ctx, dlen, dict_size, D->d_scalars + 1))) return fail_ctx(rc);
       if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
       if ((rc = hip_check(ctx, hipMemcpyAsync(D->d_scalars, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream), "copy")))
@@ -622,8 +706,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       });
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDictionaryColumn");
       c.blob = db.present ? D->d_stage + db.host_off : nullptr;
-      ORCG_ALLOC(int64_t, idx, nonnull);
-      if ((rc = int_stream(c, kSlotData, false, nonnull, idx))) return rc;
+      int64_t* idx;
+      if ((rc = int_stream(c, kSlotData, false, nonnull, &idx))) return rc;
       int64_t* ridx = idx;
       if (row_nn) {
         ORCG_ALLOC_TO(int64_t, ridx, n);
@@ -643,8 +727,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     } else {
       if (!has_len) return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDirectColumn");
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDirectColumn");
-      ORCG_ALLOC(int64_t, dlen, nonnull);
-      if ((rc = int_stream(c, kSlotLength, false, nonnull, dlen))) return rc;
+      int64_t* dlen;
+      if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen))) return rc;
       ORCG_ALLOC(int64_t, dstart, nonnull + 1);
       if ((rc = launch_exclusive_scan(ctx, dlen, nonnull, dstart))) return fail_ctx(rc);
       StreamBuf& db = c.s[kSlotData];
@@ -670,8 +754,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (!has_len)
       return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_LIST ? "LENGTH stream not found in List column"
                                                         : "LENGTH stream not found in Map column");
-    ORCG_ALLOC(int64_t, dlen, nonnull);
-    if ((rc = int_stream(c, kSlotLength, false, nonnull, dlen))) return rc;
+    int64_t* dlen;
+    if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen))) return rc;
     int64_t* rlen = dlen;
     if (row_nn) {
       ORCG_ALLOC_TO(int64_t, rlen, n);
@@ -1078,8 +1162,19 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   }
   defer_used = 0;
   checks.clear();
-  rc = decode(0, footer.stripes[hs.stripe].num_rows, nullptr, footer.stripes[hs.stripe].num_rows,
-              hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr);
+  batch.clear();
+  batched.clear();
+  const uint64_t nrows = footer.stripes[hs.stripe].num_rows;
+  const int64_t* rg_rows = hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr;
+  if (batch_on) {
+    rc = collect(0, nrows, rg_rows);
+    if (!rc && !batch.empty()) {
+      rc = launch_rlev2_multi(ctx, batch.data(), (uint32_t)batch.size());
+      if (rc) rc = fail_ctx(rc);
+    }
+  }
+  if (!rc) rc = decode(0, nrows, nullptr, nrows, rg_rows);
+  batched_streams += batch.size();
   if (rc) (void)hipStreamSynchronize(ctx->stream);  // queued copies land before the buffer is reused
   if (!rc) {
     // the checks first (in column order, as the reference raises them), then
@@ -1130,6 +1225,7 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   hipSetDevice(ctx->device);
   for (auto& t : timings) t = 0;
   stream_stats[0] = stream_stats[1] = 0;
+  batched_streams = 0;
   while (slots.size() < count) slots.emplace_back(new DevSlot());
   nslots = 0;
   if (count == 0) return ORCG_OK;
@@ -1574,6 +1670,14 @@ int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2) {
   if (!r || !out2) return ORCG_INVALID_ARGUMENT;
   out2[0] = r->stream_stats[0];
   out2[1] = r->stream_stats[1];
+  return ORCG_OK;
+}
+
+uint64_t orcg_reader_last_batched_streams(const orcg_reader* r) { return r ? r->batched_streams : 0; }
+
+int orcg_reader_set_stream_batching(orcg_reader* r, int on) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  r->batch_on = on != 0;
   return ORCG_OK;
 }
 

@@ -23,7 +23,9 @@
 //    run tables, one raw s_barrier per window. The producer never stores and
 //    the consumers never wait on vmcnt, so output stores stay in flight across
 //    windows.
+#include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include "rlev2_device.hh"
 
@@ -552,7 +554,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
       const uint32_t wt = (uint32_t)(0x40383028201E1C1Aull >> (((code - 24u) & 7u) * 8u)) & 0xffu;
       const uint32_t W = code < 24 ? code + 1u : wt;  // fbs_width
       uint32_t bits;
-      asm("s_mul_i32 %0, %1, %2" : "=s"(bits) : "s"(W), "s"(L2));
+      asm("s_mul_i32 %0, %1, %2" : "=s"(bits) : "s"(uni(W)), "s"(uni(L2)));
       rbytes = kind ? 2u + ((bits + 7u) >> 3) : 2u + ((fb >> 3) & 7u);
       rL = kind ? L2 : (fb & 7u) + 3u;
     } else {
@@ -1268,18 +1270,20 @@ __device__ __forceinline__ uint32_t* s_dense_mark(DenseLds<kDense>& d) {
 
 // Deferral (kDefer): a serial-walk instance (kDefer = 1) whose probe pass
 // finds short runs stops at the end of that pass and queues {segment, byte
-// offset, value index} in `defer_q` (two counts, then 3 words per entry);
+// offset, value index} in `defer_q` (two counts, two cursors, then 3 words per entry);
 // the dense instance launched right after it (kDefer = 2) drains the queue
 // with a persistent grid, so a short-run segment never runs the one-wave
 // header walk, whatever the stream's overall density. Launches alternate
 // between the two counts (`defer_par`): the drain of launch k zeroes the
 // count launch k + 1 will use, one store instead of a grid-wide handshake.
-template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMinWaves, int kDense = 0, int kDefer = 0>
+template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMinWaves, int kDense = 0, int kDefer = 0,
+          bool kMulti = false>
 __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
-    const uint8_t* __restrict__ src, uint64_t src_len, int is_signed,
-    const uint64_t* __restrict__ segtab, uint64_t nsegs, uint64_t rows_per_group,
-    uint64_t value_begin, uint64_t nvalues, T* __restrict__ dst, unsigned long long* err,
-    unsigned long long* __restrict__ defer_q, uint32_t defer_par) {
+    const uint8_t* __restrict__ p_src, uint64_t p_src_len, int p_is_signed,
+    const uint64_t* __restrict__ p_segtab, uint64_t p_nsegs, uint64_t rows_per_group,
+    uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* err,
+    unsigned long long* __restrict__ defer_q, uint32_t defer_par, const RleJob* __restrict__ jobs,
+    uint32_t njobs) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
@@ -1326,10 +1330,41 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
 
   const int tid = (int)threadIdx.x;
   const int wave = tid / kWave, lane = tid % kWave;
-  const uint64_t value_end = value_begin + nvalues;
+  // the stream of the segment being decoded: the launch's, or (multi-stream
+  // instances, kMulti) the job of `jobs` that owns the launch-wide segment
+  // index (single-stream instances never rebind: the arguments stay as they
+  // are, scalar and rematerialisable)
+  const uint8_t* src = p_src;
+  uint64_t src_len = p_src_len;
+  int is_signed = p_is_signed;
+  const uint64_t* segtab = p_segtab;
+  uint64_t nsegs = p_nsegs;
+  uint64_t value_begin = p_value_begin;
+  uint64_t value_end = p_value_begin + p_nvalues;
+  T* dst = p_dst;
+  auto bind = [&](const uint64_t gg) -> uint64_t {
+    if constexpr (!kMulti) return gg;
+    uint32_t lo = 0, hi = njobs - 1;
+    while (lo < hi) {  // last job whose first segment is <= gg
+      const uint32_t mid = (lo + hi + 1) >> 1;
+      if (uni64(jobs[mid].seg_base) <= gg) lo = mid;
+      else hi = mid - 1;
+    }
+    const RleJob* J = jobs + lo;
+    src = (const uint8_t*)uni64((uint64_t)(uintptr_t)J->src);
+    src_len = uni64(J->src_len);
+    is_signed = (int)uni(J->is_signed);
+    segtab = (const uint64_t*)uni64((uint64_t)(uintptr_t)J->segtab);
+    nsegs = uni64(J->nsegs);
+    value_begin = 0;
+    value_end = uni64(J->nvalues);
+    dst = (T*)uni64((uint64_t)(uintptr_t)J->dst);
+    return gg - uni64(J->seg_base);
+  };
 
   // one segment, from its start or (queued) from a byte offset / value index
-  auto run_segment = [&](const uint64_t g, const bool queued, const uint64_t q_pos, const uint64_t q_vi) {
+  auto run_segment = [&](const uint64_t gg, const bool queued, const uint64_t q_pos, const uint64_t q_vi) {
+  const uint64_t g = bind(gg);
   const uint64_t seg_start = queued ? q_pos : segtab[2 * g];
   uint64_t vi = queued ? q_vi : (kPositions ? g * rows_per_group - segtab[2 * g + 1] : segtab[2 * g + 1]);
   uint64_t seg_end = src_len;
@@ -1488,10 +1523,13 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             if (lane == 0) k = atomicAdd(s_claim, 1u);
             k = uni(k);
             uint32_t pub;
-            for (;;) {
+            // waiting waves back off: polling shares the CU's scalar unit with
+            // the walk (a short-run walk publishes an item every ~64 runs)
+            for (uint32_t spin = 0;; ++spin) {
               pub = uni(__hip_atomic_load(s_pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
               if (k < (pub & ~kWalkDone) || (pub & kWalkDone)) break;
-              __builtin_amdgcn_s_sleep(1);
+              if (spin < 2) __builtin_amdgcn_s_sleep(2);
+              else __builtin_amdgcn_s_sleep(24);
             }
             if (k >= (pub & ~kWalkDone)) break;  // the walk is done and every item is claimed
             const uint32_t e = uni(s_items[k]);
@@ -1527,9 +1565,9 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           if (was_probe && n >= 8 && dpos / n < kToDense && pos < seg_end && vi < value_end) {
             if (tid == 0) {
               const unsigned long long slot = atomicAdd(&defer_q[defer_par], 1ull);
-              defer_q[2 + 3 * slot] = g;
-              defer_q[3 + 3 * slot] = pos;
-              defer_q[4 + 3 * slot] = vi;
+              defer_q[4 + 3 * slot] = gg;
+              defer_q[5 + 3 * slot] = pos;
+              defer_q[6 + 3 * slot] = vi;
             }
             return;
           }
@@ -1598,12 +1636,23 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   };
 
   if constexpr (kDefer == 2) {
-    // persistent drain of the queue; the next launch's count starts at 0
-    if (blockIdx.x == 0 && tid == 0) defer_q[defer_par ^ 1u] = 0;
+    // persistent drain of the queue, entries claimed one at a time (their
+    // costs differ); the next launch's count and cursor start at 0
+    __shared__ unsigned long long s_next;
+    if (blockIdx.x == 0 && tid == 0) {
+      defer_q[defer_par ^ 1u] = 0;
+      defer_q[2 + (defer_par ^ 1u)] = 0;
+    }
     const uint64_t count = uni64(defer_q[defer_par]);
-    for (uint64_t i = blockIdx.x; i < count; i += gridDim.x) {
-      run_segment(uni64(defer_q[2 + 3 * i]), true, uni64(defer_q[3 + 3 * i]), uni64(defer_q[4 + 3 * i]));
-      __syncthreads();  // LDS is reused by the next entry
+    // the first entry by workgroup index, the rest from the cursor (no
+    // atomics at all when the queue is short or empty)
+    for (uint64_t i = blockIdx.x; i < count;) {
+      run_segment(uni64(defer_q[4 + 3 * i]), true, uni64(defer_q[5 + 3 * i]), uni64(defer_q[6 + 3 * i]));
+      if (gridDim.x >= count) break;
+      __syncthreads();  // LDS (and s_next) are reused by the next entry
+      if (tid == 0) s_next = gridDim.x + atomicAdd(&defer_q[2 + defer_par], 1ull);
+      __syncthreads();
+      i = uni64(s_next);
     }
   } else {
     run_segment(blockIdx.x, false, 0, 0);
@@ -1626,8 +1675,9 @@ bool rlev2_variant_valid(int v) {
 }
 
 static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
-  // [0] count, [1] done, then {segment, byte offset, value index} per entry;
-  // both counts start at zero; each drain zeroes the count of the next launch
+  // [0], [1] entry counts and [2], [3] drain cursors of even / odd launches,
+  // then {segment, byte offset, value index} per entry; all start at zero;
+  // each drain zeroes the count and cursor of the next launch
   if (ctx->defer_cap < nsegs) {
     if (ctx->d_defer) {
       (void)hipStreamSynchronize(ctx->stream);
@@ -1636,8 +1686,8 @@ static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
       ctx->defer_cap = 0;
     }
     const uint64_t cap = std::max<uint64_t>(nsegs, 4096);
-    int rc = hip_check(ctx, hipMalloc(&ctx->d_defer, (2 + 3 * cap) * 8), "hipMalloc defer queue");
-    if (!rc) rc = hip_check(ctx, hipMemsetAsync(ctx->d_defer, 0, 16, ctx->stream), "defer queue reset");
+    int rc = hip_check(ctx, hipMalloc(&ctx->d_defer, (4 + 3 * cap) * 8), "hipMalloc defer queue");
+    if (!rc) rc = hip_check(ctx, hipMemsetAsync(ctx->d_defer, 0, 32, ctx->stream), "defer queue reset");
     if (rc) return rc;
     ctx->defer_cap = cap;
   }
@@ -1645,10 +1695,26 @@ static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
   return ORCG_OK;
 }
 
-int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
-                       const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
-                       uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
-                       int dst_bytes) {
+// The default's instance for a stream: by density. Wide values (>= 5 stream
+// bytes per value, e.g. W >= 40) stream best through 33 KB windows (4 WG/CU)
+// filled through registers; narrower ones through 21 KB windows (6 WG/CU);
+// both walk run headers with one wave and queue any segment whose first runs
+// are short for the dense instance. Below 1.25 B/value the stream is likely
+// made of short runs (low-cardinality columns: SHORT_REPEAT runs are 0.2-1
+// B/value): the dense instance runs it directly (parallel run discovery,
+// 8.5 KB windows, 6 WG/CU) and falls back to the serial walk inside a segment
+// whose runs are long. Measured: scripts/ab_rlev2.py, profiles/r02/sweep.md.
+static int default_variant(uint64_t src_len, uint64_t est_values) {
+  return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 4);
+}
+
+// One launch (or serial + drain pair) of instance `variant` over nsegs
+// segments of one stream, or (jobs_d) over the launch-wide segments of a
+// device job table.
+static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode, uint64_t rows_per_group,
+                        uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes, const RleJob* jobs_d,
+                        uint32_t njobs_d) {
   if (nsegs == 0 || nvalues == 0) return ORCG_OK;
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   if (dst_bytes != 8 && dst_bytes != 4 && dst_bytes != 2)
@@ -1657,31 +1723,60 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
   const int sg = is_signed ? 1 : 0;
   unsigned long long* dq = nullptr;
   uint32_t dpar = 0;
-  // the queue consumer is a persistent grid (8 workgroups per CU)
-  const unsigned drain = (unsigned)std::min<uint64_t>(nsegs, 2048);
+  // the queue consumer is a persistent grid of exactly the resident
+  // workgroups (6 per CU for the 8.5 KB dense instance): entries are dealt
+  // out statically, so a workgroup that starts late would finish late
+  if (ctx->num_cus == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    ctx->num_cus = cus;
+  }
+  const unsigned drain = (unsigned)std::min<uint64_t>(nsegs, 6ull * (uint64_t)ctx->num_cus);
 
-#define ORCG_K(T, P, O, WKB, PIPE)                                                                   \
-  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF>), grid, block, 0, ctx->stream,   \
+#define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
+  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream, \
                      d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
-                     ctx->d_err, dq, dpar)
-#define ORCG_KX(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                  \
+                     ctx->d_err, dq, dpar, jobs_d, njobs_d)
+// single-stream instances (+ the multi-stream one for the default's
+// instances, ORCG_KX; the tuning variants have none, ORCG_KX1)
+#define ORCG_KX1(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                 \
   do {                                                                              \
     constexpr int MW = MWV;                                                         \
     constexpr int DN = (int)(DNV);                                                  \
     constexpr int DF = DFV;                                                         \
     const dim3 grid(GRIDV);                                                         \
     if (dst_bytes == 8) {                                                           \
-      if (positions_mode) ORCG_K(int64_t, true, O, WKB, PIPE);                       \
-      else ORCG_K(int64_t, false, O, WKB, PIPE);                                     \
+      if (positions_mode) ORCG_K(int64_t, true, O, WKB, PIPE, false);                \
+      else ORCG_K(int64_t, false, O, WKB, PIPE, false);                              \
     } else if (dst_bytes == 4) {                                                    \
-      if (positions_mode) ORCG_K(int32_t, true, O, WKB, PIPE);                       \
-      else ORCG_K(int32_t, false, O, WKB, PIPE);                                     \
+      if (positions_mode) ORCG_K(int32_t, true, O, WKB, PIPE, false);                \
+      else ORCG_K(int32_t, false, O, WKB, PIPE, false);                              \
     } else {                                                                        \
-      if (positions_mode) ORCG_K(int16_t, true, O, WKB, PIPE);                       \
-      else ORCG_K(int16_t, false, O, WKB, PIPE);                                     \
+      if (positions_mode) ORCG_K(int16_t, true, O, WKB, PIPE, false);                \
+      else ORCG_K(int16_t, false, O, WKB, PIPE, false);                              \
     }                                                                               \
   } while (0)
-#define ORCG_KT(O, WKB, PIPE, MWV, DNV) ORCG_KX(O, WKB, PIPE, MWV, DNV, 0, (unsigned)nsegs)
+#define ORCG_KX(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                  \
+  do {                                                                              \
+    constexpr int MW = MWV;                                                         \
+    constexpr int DN = (int)(DNV);                                                  \
+    constexpr int DF = DFV;                                                         \
+    const dim3 grid(GRIDV);                                                         \
+    if (jobs_d) {                                                                   \
+      ORCG_K(int64_t, false, O, WKB, PIPE, true);                                   \
+    } else if (dst_bytes == 8) {                                                    \
+      if (positions_mode) ORCG_K(int64_t, true, O, WKB, PIPE, false);                \
+      else ORCG_K(int64_t, false, O, WKB, PIPE, false);                              \
+    } else if (dst_bytes == 4) {                                                    \
+      if (positions_mode) ORCG_K(int32_t, true, O, WKB, PIPE, false);                \
+      else ORCG_K(int32_t, false, O, WKB, PIPE, false);                              \
+    } else {                                                                        \
+      if (positions_mode) ORCG_K(int16_t, true, O, WKB, PIPE, false);                \
+      else ORCG_K(int16_t, false, O, WKB, PIPE, false);                              \
+    }                                                                               \
+  } while (0)
+#define ORCG_KT(O, WKB, PIPE, MWV, DNV) ORCG_KX1(O, WKB, PIPE, MWV, DNV, 0, (unsigned)nsegs)
 
   // the default's instances
   constexpr int kSer = kOptNTStore | kOptReuse | kOptFast | kOptT4;  // serial-walk paths
@@ -1697,21 +1792,6 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
     ORCG_KX(kSer, 8, false, 6, 2, 2, drain);                                         \
   } while (0)
 
-  int variant = ctx->rlev2_variant;
-  if (variant == 0) {
-    // By stream density: wide values (>= 5 stream bytes per value, e.g.
-    // W >= 40) stream best through 33 KB windows (4 WG/CU) filled through
-    // registers; narrower ones through 21 KB windows (6 WG/CU); both walk
-    // run headers with one wave and queue any segment whose first runs are
-    // short for the dense instance. Below 1.25 B/value the stream is likely
-    // made of short runs (low-cardinality columns: SHORT_REPEAT runs are
-    // 0.2-1 B/value): the dense instance runs it directly (parallel run
-    // discovery, 8.5 KB windows, 6 WG/CU) and falls back to the serial walk
-    // inside a segment whose runs are long. Measured: scripts/ab_rlev2.py,
-    // profiles/r02/sweep.md.
-    const uint64_t est_values = positions_mode ? nsegs * rows_per_group : nvalues;
-    variant = src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 4);
-  }
   switch (variant) {
     case 2: ORCG_DEFERRING(kWide, 33, 1); break;            // 33 KB register-filled serial + dense drain
     case 3: ORCG_DEFERRING(kSer, 21, 6); break;             // 21 KB serial + dense drain
@@ -1741,8 +1821,86 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
 #undef ORCG_DEFERRING
 #undef ORCG_KT
 #undef ORCG_KX
+#undef ORCG_KX1
 #undef ORCG_K
   return hip_check(ctx, hipGetLastError(), "rlev2_tiled_kernel launch");
+}
+
+int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
+                       const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
+                       uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
+                       int dst_bytes) {
+  int variant = ctx->rlev2_variant;
+  if (variant == 0) variant = default_variant(src_len, positions_mode ? nsegs * rows_per_group : nvalues);
+  return launch_tiled(ctx, variant, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode, rows_per_group,
+                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0);
+}
+
+// Job tables go through a pinned ring mirrored on the device: entries are
+// reused only after the stream has drained (a wrap synchronises first).
+static int stage_jobs(Ctx* ctx, const RleJob* jobs, uint32_t n, const RleJob** out) {
+  if (ctx->jobs_cap < n) {
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_jobs) (void)hipFree(ctx->d_jobs);
+    if (ctx->h_jobs) (void)hipHostFree(ctx->h_jobs);
+    ctx->d_jobs = ctx->h_jobs = nullptr;
+    ctx->jobs_cap = ctx->jobs_used = 0;
+    const uint64_t cap = std::max<uint64_t>(4 * (uint64_t)n, 1024);
+    int rc = hip_check(ctx, hipMalloc(&ctx->d_jobs, cap * sizeof(RleJob)), "hipMalloc job table");
+    if (!rc) rc = hip_check(ctx, hipHostMalloc(&ctx->h_jobs, cap * sizeof(RleJob), hipHostMallocDefault),
+                            "hipHostMalloc job table");
+    if (rc) return rc;
+    ctx->jobs_cap = cap;
+  }
+  if (ctx->jobs_used + n > ctx->jobs_cap) {
+    int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "job ring wrap");
+    if (rc) return rc;
+    ctx->jobs_used = 0;
+  }
+  RleJob* h = (RleJob*)ctx->h_jobs + ctx->jobs_used;
+  RleJob* d = (RleJob*)ctx->d_jobs + ctx->jobs_used;
+  memcpy(h, jobs, n * sizeof(RleJob));
+  ctx->jobs_used += n;
+  *out = d;
+  return hip_check(ctx, hipMemcpyAsync(d, h, n * sizeof(RleJob), hipMemcpyHostToDevice, ctx->stream), "H2D jobs");
+}
+
+int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
+  const int pinned = ctx->rlev2_variant;
+  if (pinned == ORCG_RLEV2_WAVE_WALK || (pinned != 0 && (pinned < 2 || pinned > 5))) {
+    // not a multi-stream instance: one launch per stream
+    for (uint32_t j = 0; j < njobs; ++j) {
+      const RleJob& J = jobs[j];
+      int rc = launch_rlev2(ctx, J.src, J.src_len, (int)J.is_signed, J.segtab, J.nsegs, false, 0, 0, J.nvalues,
+                            J.dst, 8);
+      if (rc) return rc;
+    }
+    return ORCG_OK;
+  }
+  // one launch per instance: group the streams by the instance they get
+  std::vector<RleJob> group[6];
+  for (uint32_t j = 0; j < njobs; ++j) {
+    const RleJob& J = jobs[j];
+    if (J.nsegs == 0 || J.nvalues == 0) continue;
+    group[pinned ? pinned : default_variant(J.src_len, J.nvalues)].push_back(J);
+  }
+  for (int v = 2; v <= 5; ++v) {
+    std::vector<RleJob>& g = group[v];
+    if (g.empty()) continue;
+    uint64_t segs = 0, values = 0;
+    for (RleJob& J : g) {
+      J.seg_base = segs;
+      segs += J.nsegs;
+      values += J.nvalues;
+    }
+    if (segs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
+    const RleJob* d = nullptr;
+    int rc = stage_jobs(ctx, g.data(), (uint32_t)g.size(), &d);
+    if (!rc) rc = launch_tiled(ctx, v, nullptr, 0, 0, nullptr, segs, false, 0, 0, values, nullptr, 8, d,
+                               (uint32_t)g.size());
+    if (rc) return rc;
+  }
+  return ORCG_OK;
 }
 
 }  // namespace orcg

@@ -402,7 +402,13 @@ class Reader:
         """RLE streams of the last read cut by the row index / by host plans."""
         t = (ctypes.c_uint64 * 2)()
         check(self._L.orcg_reader_last_stream_stats(self._h, t))
-        return {"row_index": t[0], "host_plan": t[1]}
+        return {"row_index": t[0], "host_plan": t[1],
+                "batched": int(self._L.orcg_reader_last_batched_streams(self._h))}
+
+    def set_stream_batching(self, on=True):
+        """Decode a stripe's host-countable RLEv2 streams with one launch per
+        kernel instance (default) or one launch per stream."""
+        check(self._L.orcg_reader_set_stream_batching(self._h, int(bool(on))), self._err)
 
     def read(self, fields=None):
         """All rows as dicts of the root struct's fields (pyarrow to_pylist shape)."""

@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-copy", action="store_true", help="also time decode + D2H into host batches")
+    ap.add_argument("--no-batch", action="store_true", help="one RLEv2 launch per stream (no multi-stream launches)")
     args = ap.parse_args()
     maker, default_rows, desc = WORKLOADS[args.workload]
     rows = args.rows or default_rows
@@ -99,6 +100,8 @@ def main():
 
     ctx = orc_amd.Context(local_rank)
     r = orc_amd.Reader(path, ctx)
+    if args.no_batch:
+        r.set_stream_batching(False)
     nrows = r.num_rows
     fsize = os.path.getsize(path)
     ranges, stripe_rows = reader_ranges(r, world)

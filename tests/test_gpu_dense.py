@@ -100,8 +100,12 @@ def test_dense_streams_vs_oracle(signed, long_every):
             orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, signed, out)
             ctx.synchronize()
             got = out.cpu().numpy()
-            assert np.array_equal(got, v), "variant %d stride %d: first mismatch at %d" % (
-                variant, stride, int(np.argmax(got != v)))
+            if not np.array_equal(got, v):
+                bad = np.flatnonzero(got != v)
+                i = int(bad[0])
+                raise AssertionError("variant %d stride %d: %d mismatches, first at %d; got %s want %s" % (
+                    variant, stride, bad.size, i, got[max(0, i - 4):i + 12].tolist(),
+                    v[max(0, i - 4):i + 12].tolist()))
     ctx.set_rlev2_variant(0)
 
 

@@ -81,3 +81,29 @@ def test_workload_pipelined_read_matches_single_stripe_reads(ctx, files, name):
                         np.testing.assert_array_equal(got[m], col.data[m])
                 else:
                     np.testing.assert_array_equal(got, col.data)
+
+
+@pytest.mark.parametrize("name", ["c4", "c5"])
+def test_workload_stream_batching(ctx, files, name):
+    """A stripe's host-countable RLEv2 streams go through multi-stream
+    launches (one per kernel instance); the per-stream path (batching off)
+    decodes the same file to the same values."""
+    import pyarrow.orc as po
+
+    path = files[name]
+    f = po.ORCFile(path)
+    on = orc_amd.Reader(path, ctx)
+    off = orc_amd.Reader(path, ctx)
+    off.set_stream_batching(False)
+    last = on.num_stripes - 1
+    for s in (0, last):
+        compare_stripe(on, on.read_stripe(s), f.read_stripe(s), "%s stripe %d (batched)" % (name, s))
+        # c5: every column under the root has a PRESENT stream (its value
+        # counts come from the device), so nothing is batched there
+        assert (on.last_stream_stats()["batched"] > 0) == (name == "c4")
+        compare_stripe(off, off.read_stripe(s), f.read_stripe(s), "%s stripe %d (per stream)" % (name, s))
+        assert off.last_stream_stats()["batched"] == 0
+    if name == "c4":
+        # every integer / length / dictionary stream of the flat schema
+        on.read_stripes_device(0, 1)
+        assert on.last_stream_stats()["batched"] >= 12
