@@ -29,6 +29,8 @@ if PROF:
     FLAGS.append("-DORCG_PHASE_PROF")
 if PROF or AB:
     FLAGS.append("-DORCG_AB_VARIANTS")
+    # experiment knobs of the A/B build (e.g. ORCG_AB_FLAGS="-DORCG_ITEM_MAX=1")
+    FLAGS.extend(os.environ.get("ORCG_AB_FLAGS", "").split())
 
 
 def _mtime(p):

@@ -59,13 +59,19 @@ struct Ctx {
   uint64_t jobs_cap = 0, jobs_used = 0;
 };
 
-// One RLEv2 stream of a multi-stream launch: its bytes, segment table
-// ({byte offset, value index} per segment), output (int64) and value count;
-// seg_base = the launch-wide index of its first segment (set by the launcher).
+// One RLEv2 stream of a multi-stream launch: its bytes, segments, output
+// (int64) and value count; seg_base = the launch-wide index of its first
+// segment (set by the launcher). Segments are either a table ({byte offset,
+// value index} per segment) or, for row-index streams of a column without
+// nulls, the row index itself: {byte offset, values to skip, bits} triplets
+// (trip) and the first row of each row group (rows): value index = rows[g] -
+// skip, clamped at 0, as rg_segtab_kernel computes it.
 struct RleJob {
   const uint8_t* src;
   uint64_t src_len;
   const uint64_t* segtab;
+  const int64_t* trip;
+  const int64_t* rows;
   uint64_t nsegs;
   void* dst;
   uint64_t nvalues;

@@ -466,17 +466,25 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
   if (count == 0 || !sb.present) return ORCG_OK;
   if (!force_v2 && (c.encoding == kDirect || c.encoding == kDictionary)) return ORCG_OK;
   if (!sb.pos && count > sb.plan->values) return ORCG_OK;
-  const uint64_t* d_seg;
-  uint64_t nseg;
-  int rc = segments(c, slot, false, &d_seg, &nseg);
-  if (rc) return rc;
+  RleJob j{};
+  if (sb.pos && cur_rows) {
+    // the row index is the segment table (no rg_segtab launch): collect()
+    // only queues columns whose rows are all values (no mask)
+    j.trip = (const int64_t*)(D->d_stage + sb.rg_off);
+    j.rows = cur_rows;
+    j.nsegs = H->ngroups;
+  } else {
+    const uint64_t* d_seg;
+    uint64_t nseg;
+    int rc = segments(c, slot, false, &d_seg, &nseg);
+    if (rc) return rc;
+    j.segtab = d_seg;
+    j.nsegs = nseg;
+  }
   int64_t* out = alloc<int64_t>(count);
   if (!out) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
-  RleJob j{};
   j.src = D->d_stage + sb.host_off;
   j.src_len = sb.len;
-  j.segtab = d_seg;
-  j.nsegs = nseg;
   j.dst = out;
   j.nvalues = count;
   j.is_signed = is_signed ? 1u : 0u;

@@ -23,6 +23,7 @@
 //    run tables, one raw s_barrier per window. The producer never stores and
 //    the consumers never wait on vmcnt, so output stores stay in flight across
 //    windows.
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -87,6 +88,21 @@ constexpr int kOptReuse = 4;    // carry the window tail over in LDS; never load
 constexpr int kOptFast = 8;     // predicate-free paths for full (512-value) runs inside the output range
 constexpr int kOptRegFill = 16; // fill windows through registers (16 B buffer loads, then LDS writes), not LDS-DMA
 constexpr int kOptT4 = 32;      // walk reads DELTA varint ends from per-dword terminator nibbles computed at slice load
+
+// Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
+// counts the values of the runs it expands; each pass checks the count
+// against the values its discovery consumed.
+#ifdef ORCG_DEBUG_COVER
+#define ORCG_COVER_ADD(x) atomicAdd(s_cover_ptr(), (uint32_t)(x))
+__device__ __forceinline__ uint32_t* s_cover_ptr() {
+  __shared__ uint32_t s_cover;
+  return &s_cover;
+}
+#else
+#define ORCG_COVER_ADD(x) \
+  do {                    \
+  } while (0)
+#endif
 
 template <int kOpt, typename T>
 __device__ __forceinline__ void store1(T* p, uint64_t v) {
@@ -419,13 +435,17 @@ __device__ __forceinline__ void fill(uint32_t* win, __amdgpu_buffer_rsrc_t rs, u
 }
 
 struct WalkResult {
-  uint32_t n, stop, dpos, dval, items;
+  uint32_t n, stop, dpos, dval, items, shrt;  // shrt: stopped by the probe (short runs)
 };
 
 // Work items of a serial pass (the walk publishes item ends): a group of up
 // to 64 consecutive short runs, expanded one lane per run, or one long /
 // PATCHED_BASE run (flag kItemLong), expanded by a whole wave.
 constexpr uint16_t kItemLong = 0x8000;
+#ifndef ORCG_ITEM_MAX
+#define ORCG_ITEM_MAX 64
+#endif
+constexpr uint32_t kItemMax = ORCG_ITEM_MAX;  // short runs per group (<= 64)
 
 // The serial walk's view of a run: bytes, values and the error parse_run
 // would report, in its order. SHORT_REPEAT / DIRECT from the first two
@@ -510,7 +530,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
                                            uint64_t src_len, uint64_t value_end, int is_signed,
                                            unsigned long long* err, int lane, uint32_t lim = kWin,
                                            uint32_t cap = kCap, uint32_t* pub = nullptr,
-                                           uint16_t* items = nullptr) {
+                                           uint16_t* items = nullptr, uint32_t probe_n = 0) {
   static_assert(kCap < kItemLong, "run indices must leave the item flag free");
   constexpr uint32_t kChunk = kWin - kMaxRun;
   // everything wave-uniform and 32-bit, relative to the window / the first
@@ -520,7 +540,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
   const uint32_t a_src = src_len - wpos < 0xfffff000ull ? (uint32_t)(src_len - wpos) : 0xfffff000u;
   const uint32_t v_lim = value_end - vi < 0xffffffffull ? (uint32_t)(value_end - vi) : 0xffffffffu;
   uint32_t lp = sp, vr = 0;
-  uint32_t n = 0, stop = 0;
+  uint32_t n = 0, stop = 0, shrt = 0;
   LaneWin hw;
   hw.load(win, sp, kWin / 4 + 8, lane);
   // run k waits in lane k % 64 (r_off, r_val) until the table write of its
@@ -572,12 +592,12 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
       stop = 1;
       break;
     }
-    const uint32_t slot = n & (kWave - 1);
-    // (the lane select goes through m0: one scalar operand per VALU op)
-    asm volatile("s_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
-                 : "+v"(r_off), "+v"(r_val)
-                 : "s"(uni(lp)), "s"(uni(vr)), "s"(uni(slot))
-                 : "m0");
+    // a per-lane select, not v_writelane: the compiler may copy r_off /
+    // r_val with a partial EXEC inside a branch it cannot prove uniform, which
+    // is only safe when no lane's value is written by another lane
+    const bool mine = (uint32_t)lane == (n & (kWave - 1));
+    r_off = mine ? lp : r_off;
+    r_val = mine ? vr : r_val;
     ++n;
     lp += rbytes;
     vr += rL;
@@ -594,7 +614,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
         gstart = n;
         // expanding waves may claim the items as soon as they are published
         if (lane == 0) __hip_atomic_store(pub, nitems, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else if (n - gstart == kWave) {
+      } else if (n - gstart == kItemMax) {
         flush();
         if (lane == 0) items[nitems] = (uint16_t)n;
         ++nitems;
@@ -604,6 +624,12 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
     } else if (n - flushed == kWave) {
       flush();
     }
+    // the probe: the first probe_n runs of a segment average < kToDense
+    // bytes (a short-run segment), the caller switches to dense discovery
+    if (n == probe_n && lp - sp < probe_n * kToDense) {
+      shrt = 1;
+      break;
+    }
   }
   if (n != flushed) flush();
   if (pub && n > gstart) {
@@ -611,7 +637,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
     if (lane == 0) items[nitems] = (uint16_t)n;
     ++nitems;
   }
-  return WalkResult{n, stop, lp - sp, vr, nitems};
+  return WalkResult{n, stop, lp - sp, vr, nitems, shrt};
 }
 
 // Value j of a short run (kind SHORT_REPEAT / DIRECT / DELTA) parsed at
@@ -658,6 +684,7 @@ __device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_
                         __builtin_bswap32(__builtin_amdgcn_alignbyte(b2, b1, 1));
     uint64_t a = be >> (64 - 8 * nb);
     if (is_signed) a = unzigzag(a);
+    ORCG_COVER_ADD(L);
     for (uint32_t j = 0; __ballot(j < L) != 0; ++j) {
       const uint64_t o = o0 + j;
       if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), a);
@@ -666,6 +693,7 @@ __device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_
   }
   const Run run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
   const uint32_t L = act ? run.L : 0u;
+  ORCG_COVER_ADD(L);
   uint64_t acc = 0;
   for (uint32_t j = 0; __ballot(j < L) != 0; ++j) {
     const uint64_t o = o0 + j;
@@ -1194,6 +1222,9 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     const uint64_t bad = __ballot(!(shortr && incl <= kStage));
     const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : (uint32_t)kWave;
     if (k == 0) {
+#ifdef ORCG_DEBUG_COVER
+      if (lane == 0) ORCG_COVER_ADD(run.L);
+#endif
       expand_run<kOpt>(win, nwords, uni(s_off[c]), vi + uni(s_val[c]), is_signed, value_begin, value_end, dst, lane);
       ++c;
       continue;
@@ -1201,6 +1232,7 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     const bool mine = (uint32_t)lane < k;
     const uint32_t st0 = incl - Ls;
     const uint32_t myl = mine ? Ls : 0u;
+    ORCG_COVER_ADD(myl);
     if (__ballot(mine && run.kind != 0) == 0) {
       for (uint32_t j = 0; __ballot(j < myl) != 0; ++j)
         if (j < myl) stage[st0 + j] = run.a;
@@ -1338,6 +1370,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   uint64_t src_len = p_src_len;
   int is_signed = p_is_signed;
   const uint64_t* segtab = p_segtab;
+  const int64_t* trip = nullptr;  // multi-stream row-index jobs (RleJob::trip)
+  const int64_t* rows = nullptr;
   uint64_t nsegs = p_nsegs;
   uint64_t value_begin = p_value_begin;
   uint64_t value_end = p_value_begin + p_nvalues;
@@ -1355,6 +1389,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     src_len = uni64(J->src_len);
     is_signed = (int)uni(J->is_signed);
     segtab = (const uint64_t*)uni64((uint64_t)(uintptr_t)J->segtab);
+    trip = (const int64_t*)uni64((uint64_t)(uintptr_t)J->trip);
+    rows = (const int64_t*)uni64((uint64_t)(uintptr_t)J->rows);
     nsegs = uni64(J->nsegs);
     value_begin = 0;
     value_end = uni64(J->nvalues);
@@ -1365,14 +1401,23 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   // one segment, from its start or (queued) from a byte offset / value index
   auto run_segment = [&](const uint64_t gg, const bool queued, const uint64_t q_pos, const uint64_t q_vi) {
   const uint64_t g = bind(gg);
-  const uint64_t seg_start = queued ? q_pos : segtab[2 * g];
-  uint64_t vi = queued ? q_vi : (kPositions ? g * rows_per_group - segtab[2 * g + 1] : segtab[2 * g + 1]);
+  // segment g: {first byte, index of its first value}
+  auto seg_at = [&](const uint64_t s, uint64_t* off) -> uint64_t {
+    if (kMulti && trip) {
+      const int64_t v = rows[s] - trip[3 * s + 1];
+      *off = (uint64_t)trip[3 * s];
+      return v < 0 ? 0ull : (uint64_t)v;
+    }
+    *off = segtab[2 * s];
+    return kPositions ? s * rows_per_group - segtab[2 * s + 1] : segtab[2 * s + 1];
+  };
+  uint64_t seg_first = 0;
+  const uint64_t vi0 = queued ? 0ull : seg_at(g, &seg_first);
+  const uint64_t seg_start = queued ? q_pos : seg_first;
+  uint64_t vi = queued ? q_vi : vi0;
   uint64_t seg_end = src_len;
   uint64_t v_next = ~0ull;
-  if (g + 1 < nsegs) {
-    seg_end = segtab[2 * (g + 1)];
-    v_next = kPositions ? (g + 1) * rows_per_group - segtab[2 * (g + 1) + 1] : segtab[2 * (g + 1) + 1];
-  }
+  if (g + 1 < nsegs) v_next = seg_at(g + 1, &seg_end);
   if (seg_end > src_len) seg_end = src_len;
   if (vi >= value_end || v_next <= value_begin) return;
   if (seg_start >= seg_end) {
@@ -1456,7 +1501,11 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       // every run that starts in the window's first kChunk bytes ends inside
       // it: consume them all (several passes) before moving the window
       do {
-        uint32_t n, stop, dpos, dval;
+        uint32_t n, stop, dpos, dval, shrt = 0;
+#ifdef ORCG_DEBUG_COVER
+        if (tid == 0) *s_cover_ptr() = 0;
+        __syncthreads();
+#endif
         bool was_dense = false;
         if constexpr (kDense) was_dense = dense;
         if (was_dense) {
@@ -1502,18 +1551,21 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             // the walk is the workgroup's critical path: raise its issue
             // priority over co-resident waves that are expanding
             __builtin_amdgcn_s_setprio(3);
-            // dense instances: a short first walk (the probe) measures the
-            // stream's bytes per run before committing to a mode
-            // probe pass: 32 runs (v1 dense), 4 (v2 dense), 8 (queueing serial)
-            const uint32_t cap = ((kDense || kDefer == 1) && probe) ? (kDense == 2 ? 4u : (kDefer == 1 ? 8u : 32u)) : kCap;
+            // a segment's first walk probes its first runs (4 in dense v2
+            // instances, 8 in queueing serial ones) and stops there when
+            // they are short; a long-run segment just walks on (dense v1:
+            // a separate 32-run probe pass)
+            const uint32_t probe_n = (probe && (kDense == 2 || kDefer == 1)) ? (kDense == 2 ? 4u : 8u) : 0u;
+            const uint32_t cap = (kDense == 1 && probe) ? 32u : kCap;
             const WalkResult w = walk<kWin, kCap, (kOpt & kOptT4) != 0, OffT>(s_win[0], s_off[0], s_val[0], wpos, pos, vi,
                                                                     seg_end, src_len, value_end, is_signed, err,
-                                                                    lane, need, cap, s_pub, s_items);
+                                                                    lane, need, cap, s_pub, s_items, probe_n);
             if (lane == 0) {
               s_ctl[0][0] = w.n;
               s_ctl[0][1] = w.stop;
               s_ctl[0][2] = w.dpos;
               s_ctl[0][3] = w.dval;
+              s_ctl[0][4] = w.shrt;
               __hip_atomic_store(s_pub, w.items | kWalkDone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             __builtin_amdgcn_s_setprio(0);
@@ -1534,9 +1586,17 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             if (k >= (pub & ~kWalkDone)) break;  // the walk is done and every item is claimed
             const uint32_t e = uni(s_items[k]);
             const uint32_t r0 = k ? (uni(s_items[k - 1]) & ~(uint32_t)kItemLong) : 0u;
-            if (e & kItemLong)
+            if (e & kItemLong) {
+#ifdef ORCG_DEBUG_COVER
+              if (lane == 0) {
+                const uint32_t h = uni(s_off[0][r0]);
+                ORCG_COVER_ADD(parse_run([&](uint32_t i) { return lds_byte(s_win[0], h + i); }, ~0ull, kHdrLim,
+                                         is_signed).L);
+              }
+#endif
               expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][r0]), vi + uni(s_val[0][r0]), is_signed,
                                value_begin, value_end, dst, lane);
+            }
             else
               group_expand<kOpt>(s_win[0], s_off[0], s_val[0], r0, e, vi, is_signed, value_begin, value_end, dst,
                                  lane);
@@ -1552,8 +1612,13 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           stop = uni(s_ctl[0][1]);
           dpos = uni(s_ctl[0][2]);
           dval = uni(s_ctl[0][3]);
+          shrt = uni(s_ctl[0][4]);
         }
         __syncthreads();  // the run table (and the window) are rewritten next
+#ifdef ORCG_DEBUG_COVER
+        if (tid == 0 && !stop && *s_cover_ptr() != dval) report(err, vi, was_dense ? 0x71u : 0x70u);
+        __syncthreads();
+#endif
         PROF_MARK(was_dense ? 6 : 2);
         if (stop) return;
         pos += dpos;
@@ -1562,7 +1627,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         probe = false;
         if constexpr (kDefer == 1) {
           // a short-run segment: queue the rest for the dense instance
-          if (was_probe && n >= 8 && dpos / n < kToDense && pos < seg_end && vi < value_end) {
+          if (shrt && pos < seg_end && vi < value_end) {
             if (tid == 0) {
               const unsigned long long slot = atomicAdd(&defer_q[defer_par], 1ull);
               defer_q[4 + 3 * slot] = gg;
@@ -1576,7 +1641,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           // hysteresis on the stream bytes per run of this pass
           if (n > 0) {
             const uint32_t bpr = dpos / n;
-            if (!dense && (n >= 8 || (was_probe && n >= 4)) && bpr < kToDense) dense = true;
+            if (shrt || (!dense && (n >= 8 || (was_probe && n >= 4)) && bpr < kToDense)) dense = true;
             else if (dense && bpr >= kToSerial) dense = false;
           }
         }
@@ -1735,7 +1800,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
   const unsigned drain = (unsigned)std::min<uint64_t>(nsegs, 6ull * (uint64_t)ctx->num_cus);
 
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
-  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream, \
+  hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
                      d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
                      ctx->d_err, dq, dpar, jobs_d, njobs_d)
 // single-stream instances (+ the multi-stream one for the default's
@@ -1887,6 +1952,12 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
   for (int v = 2; v <= 5; ++v) {
     std::vector<RleJob>& g = group[v];
     if (g.empty()) continue;
+    // workgroups start in index order: the streams with the most stream
+    // bytes per value (the most runs per segment, the slowest segments) first,
+    // so the launch does not end on a tail of slow segments
+    std::stable_sort(g.begin(), g.end(), [](const RleJob& a, const RleJob& b) {
+      return (double)a.src_len * (double)b.nvalues > (double)b.src_len * (double)a.nvalues;
+    });
     uint64_t segs = 0, values = 0;
     for (RleJob& J : g) {
       J.seg_base = segs;

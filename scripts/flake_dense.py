@@ -32,8 +32,11 @@ def main():
             bad_runs = 0
             for r in range(reps):
                 out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
-                orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, False, out)
-                ctx.synchronize()
+                try:
+                    orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, False, out)
+                    ctx.synchronize()
+                except Exception as e:  # a debug build's coverage check (ORCG_DEBUG_COVER)
+                    print("variant %d stride %d rep %d: device error %s" % (variant, stride, r, e), flush=True)
                 got = out.cpu().numpy()
                 if not np.array_equal(got, v):
                     bad = np.flatnonzero(got != v)
