@@ -51,6 +51,27 @@ class Context:
         raw = getattr(stream, "cuda_stream", stream)
         check(self._L.orcg_ctx_set_stream(self._h, ctypes.c_void_p(raw)))
 
+    def stream_ptr(self):
+        """The context's hipStream_t (its own non-blocking stream, or the one
+        set_stream gave it)."""
+        return int(self._L.orcg_ctx_stream(self._h) or 0)
+
+    def after_torch(self):
+        """Order the context stream after torch's current stream: kernels
+        launched next see every tensor op queued there (allocations, fills,
+        copies). The *_device wrappers below call it; the context's own
+        stream is non-blocking, so without it a kernel could overtake e.g.
+        the torch.zeros fill of its output."""
+        import torch
+
+        cur = torch.cuda.current_stream(self.device)
+        raw = self.stream_ptr()
+        if raw == cur.cuda_stream:
+            return
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        torch.cuda.ExternalStream(raw, device=self.device).wait_event(ev)
+
     def set_rlev2_variant(self, variant):
         """0 = tiled LDS kernel (default), 1 = one-wave-per-segment walk."""
         check(self._L.orcg_ctx_set_rlev2_variant(self._h, int(variant)))
@@ -245,6 +266,7 @@ def decode_device(ctx, src, segments, nvalues, is_signed, out, value_begin=0):
     """Device-resident decode with a segment table (torch tensors on the
     context's device; asynchronous on the context stream)."""
     L = _lib.load()
+    ctx.after_torch()
     check(L.orcg_rlev2_decode_device(ctx.handle, _tensor_ptr(src), src.numel(), int(bool(is_signed)),
                                      _tensor_ptr(segments), segments.shape[0], value_begin, nvalues,
                                      _tensor_ptr(out), out.element_size()), ctx.last_error)
@@ -256,6 +278,7 @@ def decode_positions_device(ctx, src, positions, rows_per_group, nvalues, is_sig
     """Device-resident decode driven by the column's row-index positions."""
     L = _lib.load()
     n = src.numel() if src_len is None else src_len
+    ctx.after_torch()
     check(L.orcg_rlev2_decode_positions_device(ctx.handle, _tensor_ptr(src), n, int(bool(is_signed)),
                                                _tensor_ptr(positions), positions.shape[0],
                                                rows_per_group, value_begin, nvalues,
@@ -371,6 +394,7 @@ def byterle_decode_device(ctx, src, segments, nvalues, out, value_begin=0, boole
     per row) decode; torch tensors, asynchronous on the context stream."""
     L = _lib.load()
     fn = L.orcg_boolrle_decode_device if boolean else L.orcg_byterle_decode_device
+    ctx.after_torch()
     check(fn(ctx.handle, _tensor_ptr(src), src.numel(), _tensor_ptr(segments), segments.shape[0], value_begin,
              nvalues, _tensor_ptr(out)), ctx.last_error)
     return out
@@ -379,6 +403,7 @@ def byterle_decode_device(ctx, src, segments, nvalues, out, value_begin=0, boole
 def scatter_not_null_device(ctx, dense, not_null, out, fill=None):
     """dense values -> non-null rows of out (null slots untouched, or `fill`)."""
     L = _lib.load()
+    ctx.after_torch()
     check(L.orcg_scatter_not_null_device(ctx.handle, _tensor_ptr(dense), _tensor_ptr(not_null), not_null.numel(),
                                          _tensor_ptr(out), out.element_size(), 0 if fill is None else 1,
                                          0 if fill is None else int(fill)), ctx.last_error)
@@ -387,6 +412,7 @@ def scatter_not_null_device(ctx, dense, not_null, out, fill=None):
 
 def dict_offsets_device(ctx, lengths, offsets):
     L = _lib.load()
+    ctx.after_torch()
     check(L.orcg_dict_offsets_device(ctx.handle, _tensor_ptr(lengths), lengths.numel(), _tensor_ptr(offsets)),
           ctx.last_error)
     return offsets
@@ -395,6 +421,7 @@ def dict_offsets_device(ctx, lengths, offsets):
 def dict_gather_device(ctx, indices, offsets, start, length, not_null=None):
     L = _lib.load()
     nn = None if not_null is None else _tensor_ptr(not_null)
+    ctx.after_torch()
     check(L.orcg_dict_gather_device(ctx.handle, _tensor_ptr(indices), indices.element_size(), nn, indices.numel(),
                                     _tensor_ptr(offsets), offsets.numel() - 1, _tensor_ptr(start),
                                     _tensor_ptr(length)), ctx.last_error)
@@ -406,6 +433,7 @@ def decimal_decode_device(ctx, src, scales, nvalues, precision, scale, out, src_
     `out` int64[nvalues] (precision <= 18) or int64[nvalues, 2] [hi, lo]."""
     L = _lib.load()
     n = src.numel() if src_len is None else src_len
+    ctx.after_torch()
     check(L.orcg_decimal_decode_device(ctx.handle, _tensor_ptr(src), n, _tensor_ptr(scales), nvalues, precision,
                                        scale, _tensor_ptr(out)), ctx.last_error)
     return out
@@ -414,6 +442,7 @@ def decimal_decode_device(ctx, src, scales, nvalues, precision, scale, out, src_
 def timestamp_decode_device(ctx, seconds, nanos, epoch=1420070400):
     """TimestampColumnReader value construction on device tensors, in place."""
     L = _lib.load()
+    ctx.after_torch()
     check(L.orcg_timestamp_decode_device(ctx.handle, _tensor_ptr(seconds), _tensor_ptr(nanos), seconds.numel(),
                                          int(epoch)), ctx.last_error)
     return seconds, nanos
