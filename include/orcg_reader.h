@@ -194,6 +194,9 @@ int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2);
  * (every stream whose value count is known on the host: one launch per
  * kernel instance per stripe instead of one per stream). */
 uint64_t orcg_reader_last_batched_streams(const orcg_reader* r);
+/* Bytes the last read uploaded: decompressed stream bytes plus row-index /
+ * plan tables, summed over its stripes. */
+uint64_t orcg_reader_last_stage_bytes(const orcg_reader* r);
 /* Multi-stream batching on (default) / off (one launch per stream; A/B). */
 int orcg_reader_set_stream_batching(orcg_reader* r, int on);
 

@@ -165,6 +165,7 @@ SIGNATURES += [
     ("orcg_reader_metadata_value", [vp, u32, ctypes.POINTER(u64)], vp),
     ("orcg_reader_set_lazy_dictionary", [vp, i32], i32),
     ("orcg_reader_last_batched_streams", [vp], u64),
+    ("orcg_reader_last_stage_bytes", [vp], u64),
     ("orcg_reader_set_stream_batching", [vp, i32], i32),
     ("orcg_reader_is_selected", [vp, u32], i32),
     ("orcg_row_reader_create", [vp, ctypes.POINTER(RowReaderOptions), ctypes.POINTER(vp)], i32),

@@ -267,6 +267,7 @@ struct orcg_reader {
   double timings[5] = {0, 0, 0, 0, 0};
   uint64_t stream_stats[2] = {0, 0};  // last read: RLE streams cut by the row index, by host plans
   uint64_t batched_streams = 0;       // last read: RLEv2 streams decoded by multi-stream launches
+  uint64_t stage_bytes = 0;           // last read: bytes uploaded (decompressed streams + plans)
 
   // Checks whose operands are device scalars (dictionary blob size, varint
   // counts, string bytes): their D2H copies are queued on the stream and the
@@ -1153,6 +1154,7 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   ds.d_stage = (uint8_t*)ds.pool.get(hs.used + 64);
   ds.d_scalars = (uint64_t*)ds.pool.get(64);
   if (!ds.d_stage || !ds.d_scalars) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  stage_bytes += hs.used;
   int rc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, hs.used, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
   if (!rc) rc = sync_ctx(ctx);
   if (rc) return fail_ctx(rc);
@@ -1234,6 +1236,7 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   for (auto& t : timings) t = 0;
   stream_stats[0] = stream_stats[1] = 0;
   batched_streams = 0;
+  stage_bytes = 0;
   while (slots.size() < count) slots.emplace_back(new DevSlot());
   nslots = 0;
   if (count == 0) return ORCG_OK;
@@ -1682,6 +1685,7 @@ int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2) {
 }
 
 uint64_t orcg_reader_last_batched_streams(const orcg_reader* r) { return r ? r->batched_streams : 0; }
+uint64_t orcg_reader_last_stage_bytes(const orcg_reader* r) { return r ? r->stage_bytes : 0; }
 
 int orcg_reader_set_stream_batching(orcg_reader* r, int on) {
   if (!r) return ORCG_INVALID_ARGUMENT;

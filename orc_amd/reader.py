@@ -403,7 +403,8 @@ class Reader:
         t = (ctypes.c_uint64 * 2)()
         check(self._L.orcg_reader_last_stream_stats(self._h, t))
         return {"row_index": t[0], "host_plan": t[1],
-                "batched": int(self._L.orcg_reader_last_batched_streams(self._h))}
+                "batched": int(self._L.orcg_reader_last_batched_streams(self._h)),
+                "stage_bytes": int(self._L.orcg_reader_last_stage_bytes(self._h))}
 
     def set_stream_batching(self, on=True):
         """Decode a stripe's host-countable RLEv2 streams with one launch per

@@ -185,6 +185,9 @@ def main():
                                              "host_plan_and_row_index": round(ph[2], 4), "h2d": round(ph[3], 4),
                                              "device_decode": round(ph[4], 4)},
             "device_decode_Mrows_per_s": round(my_rows / max(ph[4], 1e-9) / 1e6, 1),
+            # VERDICT r01 #5 target: (uploaded stream bytes + decoded bytes) / 6 TB/s
+            "device_roofline_s": round((stats["stage_bytes"] + dec_bytes) / 6e12, 5),
+            "device_vs_roofline": round(ph[4] / max((stats["stage_bytes"] + dec_bytes) / 6e12, 1e-12), 1),
             "rle_streams": stats,
             "host_batch_copy_s": None if host is None else round(host, 3),
             "check": check,
