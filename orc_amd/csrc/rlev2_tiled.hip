@@ -87,7 +87,9 @@ constexpr int kOptNTLoad = 2;   // non-temporal LDS-DMA loads of the stream
 constexpr int kOptReuse = 4;    // carry the window tail over in LDS; never load past the segment
 constexpr int kOptFast = 8;     // predicate-free paths for full (512-value) runs inside the output range
 constexpr int kOptRegFill = 16; // fill windows through registers (16 B buffer loads, then LDS writes), not LDS-DMA
-constexpr int kOptT4 = 32;      // walk reads DELTA varint ends from per-dword terminator nibbles computed at slice load
+constexpr int kOptT4 = 32;
+constexpr int kOptD3 = 64;      // dense discovery: predicated chain marks, wave-reduced control atomics, inline probe
+constexpr int kOptDirect = 128; // dense expansion: lanes store their short runs' values straight to the output (no stage)      // walk reads DELTA varint ends from per-dword terminator nibbles computed at slice load
 
 // Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
 // counts the values of the runs it expands; each pass checks the count
@@ -530,7 +532,8 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
                                            uint64_t src_len, uint64_t value_end, int is_signed,
                                            unsigned long long* err, int lane, uint32_t lim = kWin,
                                            uint32_t cap = kCap, uint32_t* pub = nullptr,
-                                           uint16_t* items = nullptr, uint32_t probe_n = 0) {
+                                           uint16_t* items = nullptr, uint32_t probe_n = 0,
+                                           bool probe_values = false) {
   static_assert(kCap < kItemLong, "run indices must leave the item flag free");
   constexpr uint32_t kChunk = kWin - kMaxRun;
   // everything wave-uniform and 32-bit, relative to the window / the first
@@ -626,7 +629,8 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
     }
     // the probe: the first probe_n runs of a segment average < kToDense
     // bytes (a short-run segment), the caller switches to dense discovery
-    if (n == probe_n && lp - sp < probe_n * kToDense) {
+    // (probe_values: their values average <= kShortL, whatever their bytes)
+    if (n == probe_n && (probe_values ? vr <= probe_n * kShortL : lp - sp < probe_n * kToDense)) {
       shrt = 1;
       break;
     }
@@ -943,7 +947,7 @@ __device__ __forceinline__ uint32_t fbs_width_nb(uint32_t code) {
   return code < 24 ? code + 1 : hi;
 }
 
-template <typename OffT>
+template <int kOpt, typename OffT>
 __device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT* s_off, uint32_t* s_val,
                                                        uint16_t* s_nxt, uint32_t* s_mark, uint32_t* s_ctl,
                                                        uint64_t wpos, uint32_t sb, uint32_t lim, uint64_t vi,
@@ -1063,8 +1067,12 @@ __device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT
 #pragma unroll
       for (int e = 0; e < (int)kBlk; ++e) {
         const bool go = ((m8 >> e) & 1u) && na[e] != kSink;
-        const uint32_t n = go ? na[e] : 0u;
-        atomicOr(&s_mark[n >> 5], go ? 1u << (n & 31u) : 0u);
+        if constexpr ((kOpt & kOptD3) != 0) {
+          if (go) atomicOr(&s_mark[na[e] >> 5], 1u << (na[e] & 31u));
+        } else {
+          const uint32_t n = go ? na[e] : 0u;
+          atomicOr(&s_mark[n >> 5], go ? 1u << (n & 31u) : 0u);
+        }
       }
     }
 #pragma unroll
@@ -1153,7 +1161,12 @@ __device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT
     v_end = v;
     s_ctl[14] = cnt;
   }
-  if (has) {
+  if constexpr ((kOpt & kOptD3) != 0) {
+    // one atomic per wave: its first stopped lane, its last lane with an entry
+    const uint64_t bs = __ballot(has && stopped), bh = __ballot(has);
+    if (bs && lane == __builtin_ctzll(bs)) atomicMin(&s_ctl[12], (uint32_t)tid);
+    if (bh && lane == 63 - __builtin_clzll(bh)) atomicMax(&s_ctl[13], (uint32_t)tid);
+  } else if (has) {
     if (stopped) atomicMin(&s_ctl[12], (uint32_t)tid);
     atomicMax(&s_ctl[13], (uint32_t)tid);
   }
@@ -1219,7 +1232,8 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     const bool shortr = act && run.kind != 2 && run.L <= kShortL;
     const uint32_t Ls = shortr ? run.L : 0u;
     const uint32_t incl = wave_scan_u32(Ls);
-    const uint64_t bad = __ballot(!(shortr && incl <= kStage));
+    constexpr bool kStraight = (kOpt & kOptDirect) != 0;
+    const uint64_t bad = __ballot(!(shortr && (kStraight || incl <= kStage)));
     const uint32_t k = bad ? (uint32_t)__builtin_ctzll(bad) : (uint32_t)kWave;
     if (k == 0) {
 #ifdef ORCG_DEBUG_COVER
@@ -1233,6 +1247,25 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     const uint32_t st0 = incl - Ls;
     const uint32_t myl = mine ? Ls : 0u;
     ORCG_COVER_ADD(myl);
+    if constexpr (kStraight) {
+      // each lane stores its run's values at their output positions
+      const uint64_t g0 = vi + val;
+      if (__ballot(mine && run.kind != 0) == 0) {
+        for (uint32_t j = 0; __ballot(j < myl) != 0; ++j) {
+          const uint64_t g = g0 + j;
+          if (j < myl && g >= value_begin && g < value_end) store1<kOpt>(dst + (g - value_begin), run.a);
+        }
+      } else {
+        uint64_t acc = 0;
+        for (uint32_t j = 0; __ballot(j < myl) != 0; ++j) {
+          const uint64_t g = g0 + j;
+          const uint64_t x = j < myl ? short_value(win, run, hoff, j, is_signed, acc) : 0ull;
+          if (j < myl && g >= value_begin && g < value_end) store1<kOpt>(dst + (g - value_begin), x);
+        }
+      }
+      c += k;
+      continue;
+    }
     if (__ballot(mine && run.kind != 0) == 0) {
       for (uint32_t j = 0; __ballot(j < myl) != 0; ++j)
         if (j < myl) stage[st0 + j] = run.a;
@@ -1447,6 +1480,13 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     // whose bytes per run pick the mode
     bool dense = queued;
     bool probe = !queued;
+    if constexpr (kDense == 2 && (kOpt & kOptD3) != 0) {
+      // queued segments (short runs by values) are sized by the inline
+      // probe too: dense discovery for short runs in bytes, the serial walk
+      // with staged group expansion for wide ones
+      dense = false;
+      probe = true;
+    }
     while (pos < seg_end && vi < value_end) {
       const uint32_t wrel = (uint32_t)(pos - bias) & ~15u;
       const uint64_t wpos = bias + wrel;
@@ -1498,6 +1538,26 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       PROF_MARK(0);
+      if constexpr (kDense == 2 && (kOpt & kOptD3) != 0) {
+        // inline probe (no serial pass): one lane sizes the segment's first
+        // runs; short ones (< kToDense stream bytes each) start it dense
+        if (probe) {
+          if (tid == 0) {
+            uint32_t p = (uint32_t)(pos - wpos), nb = 0, nr = 0;
+            while (nr < 4 && nb < 4 * kToDense && p + kHdrLim < need) {
+              const Run r = parse_run([&](uint32_t i) { return lds_byte(s_win[0], p + i); }, ~0ull, kHdrLim, is_signed);
+              if (r.err != kErrNone || r.kind == 2) break;
+              nb += r.bytes;
+              p += r.bytes;
+              ++nr;
+            }
+            s_ctl[0][15] = (nr == 4 && nb < 4 * kToDense) ? 1u : 0u;
+          }
+          __syncthreads();
+          dense = uni(s_ctl[0][15]) != 0;
+          probe = false;
+        }
+      }
       // every run that starts in the window's first kChunk bytes ends inside
       // it: consume them all (several passes) before moving the window
       do {
@@ -1513,7 +1573,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           const uint32_t lim = min(kSlab, kChunk - sb);
           DenseResult d;
           if constexpr (kDense == 2) {
-            d = dense2_discover(s_win[0], s_off[0], s_val[0], s_nxt2, s_mark2, s_ctl[0], wpos, sb, lim, vi, seg_end,
+            d = dense2_discover<kOpt>(s_win[0], s_off[0], s_val[0], s_nxt2, s_mark2, s_ctl[0], wpos, sb, lim, vi, seg_end,
                                 src_len, value_end, need, is_signed, err, tid
 #ifdef ORCG_PHASE_PROF
                                 , prof_last_
@@ -1556,10 +1616,12 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             // they are short; a long-run segment just walks on (dense v1:
             // a separate 32-run probe pass)
             const uint32_t probe_n = (probe && (kDense == 2 || kDefer == 1)) ? (kDense == 2 ? 4u : 8u) : 0u;
+            constexpr bool kProbeValues = kDefer == 1 && (kOpt & kOptD3) != 0;
             const uint32_t cap = (kDense == 1 && probe) ? 32u : kCap;
             const WalkResult w = walk<kWin, kCap, (kOpt & kOptT4) != 0, OffT>(s_win[0], s_off[0], s_val[0], wpos, pos, vi,
                                                                     seg_end, src_len, value_end, is_signed, err,
-                                                                    lane, need, cap, s_pub, s_items, probe_n);
+                                                                    lane, need, cap, s_pub, s_items, probe_n,
+                                                                    kProbeValues);
             if (lane == 0) {
               s_ctl[0][0] = w.n;
               s_ctl[0][1] = w.stop;
@@ -1597,6 +1659,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][r0]), vi + uni(s_val[0][r0]), is_signed,
                                value_begin, value_end, dst, lane);
             }
+            else if constexpr (kDense == 2 && (kOpt & kOptD3) != 0)
+              // coalesced stores through the wave's value stage
+              dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], s_stage2 + wave * kStage, r0, e, vi,
+                                 is_signed, value_begin, value_end, dst, lane);
             else
               group_expand<kOpt>(s_win[0], s_off[0], s_val[0], r0, e, vi, is_signed, value_begin, value_end, dst,
                                  lane);
@@ -1732,7 +1798,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
 // tuning experiments of the A/B sweeps (8-24) are compiled only into the A/B
 // build (ORCG_AB=1 python -m orc_amd.build -> liborcgpu_ab.so).
 bool rlev2_variant_valid(int v) {
-  if (v >= 0 && v <= 5) return true;
+  if (v >= 0 && v <= 7) return true;
 #ifdef ORCG_AB_VARIANTS
   if (v >= 8 && v <= kMaxRlev2Variant) return true;
 #endif
@@ -1848,20 +1914,22 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
   constexpr int kWide = kSer | kOptRegFill;
   // a serial instance that queues short-run segments, then the dense
   // instance that drains the queue
-#define ORCG_DEFERRING(O, WKB, MWV)                                                   \
+#define ORCG_DEFERRING(O, WKB, MWV, DO)                                               \
   do {                                                                              \
     int rc_ = defer_queue(ctx, nsegs, &dq);                                          \
     if (rc_) return rc_;                                                            \
     dpar = (uint32_t)(ctx->defer_seq++ & 1u);                                       \
     ORCG_KX(O, WKB, false, MWV, 0, 1, (unsigned)nsegs);                              \
-    ORCG_KX(kSer, 8, false, 6, 2, 2, drain);                                         \
+    ORCG_KX(DO, 8, false, 6, 2, 2, drain);                                           \
   } while (0)
 
   switch (variant) {
-    case 2: ORCG_DEFERRING(kWide, 33, 1); break;            // 33 KB register-filled serial + dense drain
-    case 3: ORCG_DEFERRING(kSer, 21, 6); break;             // 21 KB serial + dense drain
-    case 4: ORCG_KX(kSer, 8, false, 6, 2, 0, (unsigned)nsegs); break;   // dense v2, 8.5 KB
-    case 5: ORCG_KX(kSer, 12, false, 5, 2, 0, (unsigned)nsegs); break;  // dense v2, 12.5 KB
+    case 2: ORCG_DEFERRING(kWide | kOptD3, 33, 1, kSer | kOptD3); break;  // 33 KB register-filled serial + dense drain
+    case 3: ORCG_DEFERRING(kSer | kOptD3, 21, 6, kSer | kOptD3); break;   // 21 KB serial + dense drain
+    case 4: ORCG_KX(kSer | kOptD3, 8, false, 6, 2, 0, (unsigned)nsegs); break;   // dense v3, 8.5 KB
+    case 5: ORCG_KX(kSer | kOptD3, 12, false, 5, 2, 0, (unsigned)nsegs); break;  // dense v3, 12.5 KB
+    case 6: ORCG_KX(kSer, 8, false, 6, 2, 0, (unsigned)nsegs); break;            // round-2 dense v2 (A/B)
+    case 7: ORCG_DEFERRING(kWide, 33, 1, kSer); break;                          // round-2 33 KB serial (A/B)
 #ifdef ORCG_AB_VARIANTS
     case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false); break;  // 21 KB + fast
     case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
@@ -1949,6 +2017,13 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
     if (J.nsegs == 0 || J.nvalues == 0) continue;
     group[pinned ? pinned : default_variant(J.src_len, J.nvalues)].push_back(J);
   }
+  static const bool dbg = getenv("ORCG_DEBUG_JOBS") != nullptr;
+  if (dbg)
+    for (int v = 2; v <= 5; ++v)
+      for (const RleJob& J : group[v])
+        fprintf(stderr, "rle job: instance %d bytes %llu values %llu segments %llu (%.3f B/value)\n", v,
+                (unsigned long long)J.src_len, (unsigned long long)J.nvalues, (unsigned long long)J.nsegs,
+                (double)J.src_len / (double)J.nvalues);
   for (int v = 2; v <= 5; ++v) {
     std::vector<RleJob>& g = group[v];
     if (g.empty()) continue;

@@ -169,3 +169,65 @@ def test_dense_errors_match_reference(case, variant):
         assert str(got.value) == str(want.value)
     finally:
         ctx.set_rlev2_variant(0)
+
+
+def _wide_short_stream(rng, n_target):
+    """Short runs (1-10 values) of wide values (>= 5 stream bytes per value):
+    the serial instances queue such segments by values per run, and the
+    drain walks them serially with staged (coalesced) group expansion."""
+    vals, kinds, lens = [], [], []
+    total = 0
+    while total < n_target:
+        r = rng.random()
+        L = int(rng.integers(1, 11))
+        if r < 0.6:
+            k = 1
+            w = int(rng.integers(40, 65))
+            hi = (1 << (w - 1)) - 1
+            v = list(rng.integers(-hi - 1, hi, size=L, endpoint=True))
+        elif r < 0.8:
+            k, L = 0, max(L, 3)
+            v = [int(rng.integers(-(1 << 62), 1 << 62))] * L
+        else:
+            k = 3
+            start = int(rng.integers(-(1 << 60), 1 << 60))
+            d = rng.integers(1 << 30, 1 << 40, size=L)
+            d[0] = 0
+            v = list(start + np.cumsum(d))
+        vals += v
+        kinds.append(k)
+        lens.append(L)
+        total += L
+    return np.array(vals, dtype=np.int64), np.array(kinds, dtype=np.uint8), np.array(lens, dtype=np.uint32)
+
+
+def test_wide_short_runs_vs_oracle():
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(2026)
+    v, kinds, lens = _wide_short_stream(rng, 300_000)
+    ctx = orc_amd.default_context(0)
+    n = v.size
+    for stride in (10_000, 777):
+        data, pos = _encode_with_positions(orc_amd, v, True, kinds, lens, stride)
+        assert data.size >= 5 * n  # the >= 5 B/value instance under variant 0
+        if stride == 10_000:
+            np.testing.assert_array_equal(oracle.rlev2_decode(data.tobytes(), n, True), v)
+        d_src = torch.from_numpy(data).cuda()
+        d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+        for variant in orc_amd.rlev2_variants():
+            ctx.set_rlev2_variant(variant)
+            out = torch.zeros(n, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, n, True, out)
+            ctx.synchronize()
+            got = out.cpu().numpy()
+            assert np.array_equal(got, v), "variant %d stride %d: first mismatch at %d" % (
+                variant, stride, int(np.argmax(got != v)))
+            for a, b in [(12345, 54321), (n - 7, n)]:
+                o = torch.full((b - a,), -7, dtype=torch.int64, device="cuda")
+                orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, b - a, True, o, value_begin=a)
+                ctx.synchronize()
+                np.testing.assert_array_equal(o.cpu().numpy(), v[a:b])
+    ctx.set_rlev2_variant(0)
