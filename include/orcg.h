@@ -248,7 +248,11 @@ int orcg_dict_gather_device(orcg_ctx* ctx, const void* d_indices, int index_widt
  * nvalues values rescaled to `scale`. precision <= 18: int64 d_out[nvalues]
  * ("Decimal scale out of range" past 18 digits, readInt64 :1342-1349);
  * precision > 18: int64 d_out[2 * nvalues], [hi, lo] per value (orc::Int128).
- * Fewer varints than nvalues: "Read past end of stream in
+ * precision == 0: Hive 0.11 decimals (DecimalHive11ColumnReader, :1578-1692),
+ * Int128 layout rescaled to `scale` (the forced scale, RowReaderOptions::
+ * forcedScaleOnHive11Decimal, 6 by default); a value past 128 bits or 38
+ * digits is "Hive 0.11 decimal was more than 38 digits." (the reference's
+ * default throwOnHive11DecimalOverflow). Fewer varints than nvalues: "Read past end of stream in
  * Decimal64ColumnReader". Synchronous. */
 int orcg_decimal_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len, const int64_t* d_scales,
                                uint64_t nvalues, uint32_t precision, int32_t scale, void* d_out);

@@ -24,6 +24,7 @@
  *                                           (Decimal64VectorBatch::values)
  *   DECIMAL, precision > 18               : int64 data[2n], [hi, lo] per value (orc::Int128 layout,
  *                                           Decimal128VectorBatch::values)
+ *   DECIMAL, precision 0 (Hive 0.11)      : as precision > 18, at orcg_reader_hive11_scale()
  *   TIMESTAMP, TIMESTAMP_INSTANT          : int64 data[n] seconds (UTC), int64 secondary[n] nanoseconds
  *                                           (TimestampVectorBatch::data / nanoseconds)
  *   LIST, MAP                             : int64 offsets[n + 1] (ListVectorBatch::offsets);
@@ -37,7 +38,7 @@
  * decoding (orcg_reader_set_lazy_dictionary, RowReaderOptions::
  * setEnableLazyDecoding) only those are produced (data / length are NULL).
  * Null slots hold 0 (the reference leaves them unspecified). Not decoded
- * (view.decoded == 0): Hive 0.11 decimals (precision 0) and TIMESTAMP columns
+ * (view.decoded == 0): TIMESTAMP columns
  * whose writer time zone is not UTC (the reference converts those with the
  * IANA zone rules, Timezone.cc).
  */
@@ -140,6 +141,13 @@ int orcg_reader_is_selected(const orcg_reader* r, uint32_t type_id);
 /* RowReaderOptions::setEnableLazyDecoding: dictionary string columns decode to
  * index + dictionary only (StringDictionaryColumnReader::nextEncoded). */
 int orcg_reader_set_lazy_dictionary(orcg_reader* r, int on);
+/* RowReaderOptions::forcedScaleOnHive11Decimal / throwOnHive11DecimalOverflow
+ * (c++/include/orc/Reader.hh:258-271): Hive 0.11 decimals (precision 0) decode
+ * as Decimal128 [hi, lo] values at forced_scale (default 6); a value past 38
+ * digits raises "Hive 0.11 decimal was more than 38 digits." Only
+ * throw_on_overflow = 1 (the reference's default) is supported. */
+int orcg_reader_set_hive11_decimal(orcg_reader* r, int32_t forced_scale, int throw_on_overflow);
+int32_t orcg_reader_hive11_scale(const orcg_reader* r);
 
 /* Decode one stripe of the selected columns into device batches owned by the
  * reader (valid until the next read or destroy). Synchronous. */

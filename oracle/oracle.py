@@ -196,12 +196,13 @@ def dict_gather(indices, lengths, not_null=None):
 
 def decimal_decode(data, scales, n, scale, wide):
     """Decimal64/128ColumnReader value decode (orco_decimal_decode): int64[n],
-    or int64[n, 2] of [hi, lo] when wide."""
+    or int64[n, 2] of [hi, lo] when wide (wide=2: Hive 0.11 decimals, with the
+    38-digit check)."""
     L = lib()
     buf = np.frombuffer(bytes(data), dtype=np.uint8)
     sc = np.ascontiguousarray(scales, dtype=np.int64)
     out = np.zeros((n, 2) if wide else n, dtype=np.int64)
-    if L.orco_decimal_decode(buf.ctypes.data, buf.size, sc.ctypes.data, n, int(scale), int(bool(wide)),
+    if L.orco_decimal_decode(buf.ctypes.data, buf.size, sc.ctypes.data, n, int(scale), 2 if wide == 2 else int(bool(wide)),
                              out.ctypes.data) != 0:
         raise OracleError(L.orco_last_error().decode())
     return out

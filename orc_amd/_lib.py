@@ -164,6 +164,8 @@ SIGNATURES += [
     ("orcg_reader_metadata_key", [vp, u32], cp),
     ("orcg_reader_metadata_value", [vp, u32, ctypes.POINTER(u64)], vp),
     ("orcg_reader_set_lazy_dictionary", [vp, i32], i32),
+    ("orcg_reader_set_hive11_decimal", [vp, i32, i32], i32),
+    ("orcg_reader_hive11_scale", [vp], i32),
     ("orcg_reader_last_batched_streams", [vp], u64),
     ("orcg_reader_last_stage_bytes", [vp], u64),
     ("orcg_reader_set_stream_batching", [vp, i32], i32),

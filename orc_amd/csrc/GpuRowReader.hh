@@ -394,7 +394,8 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
   } else if (auto* d128 = dynamic_cast<Decimal128VectorBatch*>(&b)) {
     const orcg_type_info t = r_.getType(id);
     d128->precision = (int32_t)t.precision;
-    d128->scale = (int32_t)t.scale;
+    // Hive 0.11 decimals: the forced scale (DecimalHive11ColumnReader::next)
+    d128->scale = t.precision == 0 ? (int32_t)orcg_reader_hive11_scale(r_.get()) : (int32_t)t.scale;
     r_.copy(d128->values, v.data, n, first);  // [hi, lo] per value = Int128's layout
   } else if (auto* ts = dynamic_cast<TimestampVectorBatch*>(&b)) {
     r_.copy(ts->data, v.data, n, first);

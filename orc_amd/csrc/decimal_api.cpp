@@ -9,7 +9,7 @@ extern "C" {
 
 int orcg_decimal_decode_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_len, const int64_t* d_scales,
                                uint64_t nvalues, uint32_t precision, int32_t scale, void* d_out) {
-  if (!c || (src_len && !d_src) || (nvalues && (!d_scales || !d_out)) || precision == 0)
+  if (!c || (src_len && !d_src) || (nvalues && (!d_scales || !d_out)) || precision > 38)
     return ORCG_INVALID_ARGUMENT;
   (void)hipSetDevice(c->device);
   const uint64_t ntiles_max = src_len / 16384 + 2;
@@ -29,7 +29,7 @@ int orcg_decimal_decode_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_l
   }
   if (total < nvalues) return set_error(c, ORCG_PARSE_ERROR, "Read past end of stream in Decimal64ColumnReader");
   if ((rc = launch_varint_decimal(c, d_src, src_len, (const int64_t*)d_base, d_scales, nvalues, scale,
-                                  precision > 18, d_out)))
+                                  precision == 0 ? 2 : (precision > 18 ? 1 : 0), d_out)))
     return rc;
   return sync_ctx(c);
 }

@@ -118,7 +118,10 @@ __device__ __forceinline__ U128 div128_pow10(U128 v, uint32_t k) {
 }
 
 // kMode 0: Decimal64 (int64 out, readInt64); 1: Decimal128 ([hi, lo] int64
-// pairs = orc::Int128's layout, readInt128)
+// pairs = orc::Int128's layout, readInt128); 2: Hive 0.11 decimals (precision
+// 0, DecimalHive11ColumnReader::readInt128, ColumnReader.cc:1586-1617): as 1,
+// plus the 128-bit varint limit and the 38-digit range check, both reported
+// as "Hive 0.11 decimal was more than 38 digits." (throwOnHive11DecimalOverflow)
 template <int kMode>
 __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
     const uint8_t* __restrict__ src, uint64_t len, const int64_t* __restrict__ tile_base,
@@ -173,8 +176,10 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
   // terminator: look back (staged bytes first, then global memory)
   uint64_t acc_lo = 0, acc_hi = 0;
   uint32_t shift = 0;
+  bool too_long = false;  // kMode 2: more than 128 bits (:1600)
   auto push = [&](uint32_t b) {
     const uint64_t x = b & 0x7fu;
+    if constexpr (kMode == 2) too_long = too_long || shift > 128 || (shift == 126 && x > 3);
     if constexpr (kMode == 0) {
       acc_lo |= x << (shift & 63u);  // x86 shift-count masking of readInt64's UB shift
     } else {
@@ -250,6 +255,13 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
               c -= a;
             }
           }
+          if constexpr (kMode == 2) {
+            // value >= MIN_VALUE && value <= MAX_VALUE, |v| <= 10^38 - 1 (:1616)
+            const U128 m = (int64_t)v.hi < 0 ? neg128(v) : v;
+            const uint64_t kHi = 0x4B3B4CA85A86C47Aull, kLo = 0x098A223FFFFFFFFFull;
+            const bool big = m.hi > kHi || (m.hi == kHi && m.lo > kLo);
+            if (too_long || big) atomicMin(err, (unsigned long long)((k << 8) | kErrHive11Overflow));
+          }
           int64_t* o = (int64_t*)out + 2 * k;
           o[0] = (int64_t)v.hi;
           o[1] = (int64_t)v.lo;
@@ -258,6 +270,7 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
       ++k;
       acc_lo = acc_hi = 0;
       shift = 0;
+      too_long = false;
     }
   }
 }
@@ -291,10 +304,13 @@ int launch_varint_tile_counts(Ctx* ctx, const uint8_t* d_src, uint64_t len, int6
 }
 
 int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
-                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, bool wide, void* d_out) {
+                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out) {
   const uint64_t ntiles = (len + kVTile - 1) / kVTile;
   if (ntiles == 0 || nvalues == 0) return ORCG_OK;
-  if (wide)
+  if (mode == 2)
+    hipLaunchKernelGGL(varint_decimal_kernel<2>, dim3((unsigned)ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
+                       d_tile_base, d_scales, nvalues, scale, d_out, ctx->d_err);
+  else if (mode == 1)
     hipLaunchKernelGGL(varint_decimal_kernel<1>, dim3((unsigned)ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
                        d_tile_base, d_scales, nvalues, scale, d_out, ctx->d_err);
   else

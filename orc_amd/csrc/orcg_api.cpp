@@ -24,6 +24,7 @@ const char* dev_error_message(uint32_t code) {
     case kErrDictIndex: return "Entry index out of range in StringDictionaryColumn";
     case kErrV1BadRead: return "bad read in readByte";
     case kErrDecimalScale: return "Decimal scale out of range";
+    case kErrHive11Overflow: return "Hive 0.11 decimal was more than 38 digits.";
   }
   return "unknown device error";
 }

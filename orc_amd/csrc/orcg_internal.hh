@@ -25,6 +25,7 @@ enum DevErr : uint32_t {
   kErrDictIndex = 7,       // "Entry index out of range in StringDictionaryColumn" (ColumnReader.cc:578)
   kErrV1BadRead = 8,       // "bad read in readByte" (RLEv1.cc:141-146)
   kErrDecimalScale = 9,    // "Decimal scale out of range" (ColumnReader.cc:1348)
+  kErrHive11Overflow = 10, // "Hive 0.11 decimal was more than 38 digits." (ColumnReader.cc:1654)
 };
 
 const char* dev_error_message(uint32_t code);
@@ -122,7 +123,7 @@ int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t
 // int64 (Decimal64) or [hi, lo] int64 pairs (Decimal128, orc::Int128 layout).
 int launch_varint_tile_counts(Ctx* ctx, const uint8_t* d_src, uint64_t len, int64_t* d_counts, uint64_t* ntiles);
 int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
-                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, bool wide, void* d_out);
+                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out);  // mode: 0 Decimal64, 1 Decimal128, 2 Hive 0.11
 // TimestampColumnReader value construction, in place.
 int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, int64_t epoch);
 

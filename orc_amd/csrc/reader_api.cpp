@@ -88,12 +88,12 @@ constexpr int64_t kOrcEpochUtc = 1420070400;
 bool range_ok(uint64_t off, uint64_t len, uint64_t end) { return off <= end && len <= end - off; }
 
 // Columns this reader decodes: every primitive, list / map / struct / union,
-// decimals with a precision (Hive 0.11 precision-0 decimals are not),
-// timestamps of UTC writers.
+// decimals (Hive 0.11 precision-0 decimals at the forced scale), timestamps
+// of UTC writers.
 bool is_supported(const file::TypeInfo& t, const std::string& writer_tz) {
   const uint32_t k = t.kind;
   if (k == ORCG_TYPE_UNION) return true;
-  if (k == ORCG_TYPE_DECIMAL) return t.precision != 0;
+  if (k == ORCG_TYPE_DECIMAL) return true;
   if (k == ORCG_TYPE_TIMESTAMP) return utc_zone(writer_tz);
   if (k == ORCG_TYPE_TIMESTAMP_INSTANT) return true;
   return k <= ORCG_TYPE_CHAR || k == ORCG_TYPE_DATE || k == ORCG_TYPE_VARCHAR;
@@ -258,6 +258,7 @@ struct orcg_reader {
   HostStage stages[2];
   bool decimal_as_long = false;  // PostScript version 1.9999 (UNSTABLE-PRE-2.0): Decimal64V2 columns (Reader.cc:1693-1699)
   bool lazy_dict = false;
+  int32_t hive11_scale = 6;  // RowReaderOptions::forcedScaleOnHive11Decimal (Reader.cc RowReaderOptionsPrivate: 6)
   std::string software_version;  // orcg_reader_software_version's buffer  // RowReaderOptions::setEnableLazyDecoding: dictionary columns keep index + dictionary only
   std::vector<std::unique_ptr<DevSlot>> slots;  // results of the last read, in stripe order
   size_t nslots = 0;
@@ -507,7 +508,7 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
   const uint32_t k = c.kind;
   int rc = ORCG_OK;
   if (k == ORCG_TYPE_DECIMAL) {
-    if (decimal_as_long && footer.types[id].precision <= 18) rc = queue_stream(id, kSlotData, true, n, true);
+    if (decimal_as_long && footer.types[id].precision - 1u < 18u) rc = queue_stream(id, kSlotData, true, n, true);
     else rc = queue_stream(id, kSlotSecondary, true, n, false);
   } else if (k == ORCG_TYPE_TIMESTAMP || k == ORCG_TYPE_TIMESTAMP_INSTANT) {
     rc = queue_stream(id, kSlotData, true, n, false);
@@ -595,7 +596,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   if (k == ORCG_TYPE_DECIMAL) {
     const file::TypeInfo& t = footer.types[id];
     const std::string cid = std::to_string(id);
-    if (decimal_as_long && t.precision <= 18) {
+    if (decimal_as_long && t.precision - 1u < 18u) {  // precision 1..18 (0 = Hive 0.11 first)
       // Decimal64ColumnReaderV2 (ColumnReader.cc:1529-1576): RLEv2 unscaled values
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64V2 column. ColumnId=" + cid);
       int64_t* dense;
@@ -606,7 +607,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       // DATA, per-value scales in SECONDARY (signed RLE)
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64Column");
       if (!has_sec) return fail(ORCG_PARSE_ERROR, "SECONDARY stream not found in Decimal64Column");
-      const bool wide = t.precision > 18;
+      // Hive 0.11 (precision 0): Decimal128 at the forced scale (DecimalHive11ColumnReader, :1627-1687)
+      const bool hive11 = t.precision == 0;
+      const bool wide = hive11 || t.precision > 18;
       int64_t* scales;
       if ((rc = int_stream(c, kSlotSecondary, true, nonnull, &scales))) return rc;
       const StreamBuf& sb = c.s[kSlotData];
@@ -624,7 +627,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
                                 : ORCG_OK;
       });
       ORCG_ALLOC(int64_t, dense, wide ? 2 * nonnull : nonnull);
-      if ((rc = launch_varint_decimal(ctx, d_src, sb.len, base, scales, nonnull, (int32_t)t.scale, wide, dense)))
+      if ((rc = launch_varint_decimal(ctx, d_src, sb.len, base, scales, nonnull,
+                                    hive11 ? hive11_scale : (int32_t)t.scale, hive11 ? 2 : (wide ? 1 : 0), dense)))
         return fail_ctx(rc);
       if (!row_nn) {
         c.data = dense;
@@ -985,7 +989,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
           order.push_back({kSlotLength, kInt});
         }
       } else if (k == ORCG_TYPE_DECIMAL) {
-        if (decimal_as_long && footer.types[col].precision <= 18) order.push_back({kSlotData, kInt});
+        if (decimal_as_long && footer.types[col].precision - 1u < 18u) order.push_back({kSlotData, kInt});
         else {
           order.push_back({kSlotData, kRaw});
           order.push_back({kSlotSecondary, kInt});
@@ -1088,7 +1092,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
         else if (is_int_kind(c.kind) || c.kind == ORCG_TYPE_TIMESTAMP || c.kind == ORCG_TYPE_TIMESTAMP_INSTANT ||
                  (is_string_kind(c.kind) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)))
           kind = v1 ? 1 : 2;
-        else if (c.kind == ORCG_TYPE_DECIMAL && decimal_as_long && footer.types[i].precision <= 18)
+        else if (c.kind == ORCG_TYPE_DECIMAL && decimal_as_long && footer.types[i].precision - 1u < 18u)
           kind = 2;  // Decimal64ColumnReaderV2: RLEv2 (ColumnReader.cc:1544-1556)
         else continue;  // raw bytes / varints
       } else {
@@ -1433,6 +1437,13 @@ int orcg_reader_set_lazy_dictionary(orcg_reader* r, int on) {
   r->lazy_dict = on != 0;
   return ORCG_OK;
 }
+int orcg_reader_set_hive11_decimal(orcg_reader* r, int32_t forced_scale, int throw_on_overflow) {
+  if (!r || forced_scale < 0 || forced_scale > 38) return ORCG_INVALID_ARGUMENT;
+  if (!throw_on_overflow) return r->fail(ORCG_INVALID_ARGUMENT, "throwOnHive11DecimalOverflow(false) is not supported");
+  r->hive11_scale = forced_scale;
+  return ORCG_OK;
+}
+int32_t orcg_reader_hive11_scale(const orcg_reader* r) { return r ? r->hive11_scale : 6; }
 int orcg_reader_format_version(const orcg_reader* r, uint32_t* major, uint32_t* minor) {
   if (!r || !major || !minor) return ORCG_INVALID_ARGUMENT;
   // the reference reports 0.11 when the version is absent (FileVersion::v_0_11)

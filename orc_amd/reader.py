@@ -117,12 +117,13 @@ class Batch:
             return float(c.data[i])
         if k == DECIMAL:
             # Decimal64VectorBatch int64 / Decimal128VectorBatch [hi, lo]
-            if t.precision > 18:
+            # (Hive 0.11 precision-0 decimals: Decimal128 at the forced scale)
+            if t.precision > 18 or t.precision == 0:
                 hi, lo = int(c.data[2 * i]), int(c.data[2 * i + 1]) & ((1 << 64) - 1)
                 u = (hi << 64) | lo
             else:
                 u = int(c.data[i])
-            return decimal.Decimal(u).scaleb(-t.scale)
+            return decimal.Decimal(u).scaleb(-(t.scale if t.precision else self.reader.hive11_scale))
         if k in (TIMESTAMP, TIMESTAMP_INSTANT):
             # TimestampVectorBatch seconds + nanoseconds, as numpy datetime64[ns]
             return np.datetime64(int(c.data[i]) * 1_000_000_000 + int(c.secondary[i]), "ns")
@@ -342,7 +343,7 @@ class Reader:
             tags = host(v.tags, 1, np.uint8, n)
             offsets = host(v.offsets, 8, np.int64, n)
         if k == DECIMAL:
-            w = 16 if t.precision > 18 else 8
+            w = 16 if t.precision > 18 or t.precision == 0 else 8
             data = host(v.data, w, np.int64, n).reshape(-1) if w == 8 else \
                 self._host(v.data + begin * 16, 16 * n, np.int64) if n else np.zeros(0, np.int64)
         elif k in (TIMESTAMP, TIMESTAMP_INSTANT):
@@ -381,6 +382,16 @@ class Reader:
             p = self._L.orcg_reader_metadata_value(self._h, i, ctypes.byref(ln))
             out[key] = ctypes.string_at(p, ln.value) if p and ln.value else b""
         return out
+
+    def set_hive11_decimal(self, forced_scale=6, throw_on_overflow=True):
+        """RowReaderOptions::forcedScaleOnHive11Decimal /
+        throwOnHive11DecimalOverflow (only throwing is supported)."""
+        check(self._L.orcg_reader_set_hive11_decimal(self._h, int(forced_scale), int(bool(throw_on_overflow))),
+              self._err)
+
+    @property
+    def hive11_scale(self):
+        return int(self._L.orcg_reader_hive11_scale(self._h))
 
     def set_lazy_dictionary(self, on=True):
         """RowReaderOptions::setEnableLazyDecoding for stripe reads."""

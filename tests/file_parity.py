@@ -258,7 +258,7 @@ def compare_column(reader, batch, tid, arr, ours_idx, theirs_idx, where=""):
             "%s col %d (float) differs" % (where, tid)
     elif k == 14:  # decimal: unscaled values (int64, or [hi, lo] pairs past 18 digits)
         words = np.frombuffer(arr.buffers()[1], dtype=np.int64).reshape(-1, 2)[arr.offset:arr.offset + len(arr)]
-        if t.precision > 18:
+        if t.precision > 18 or t.precision == 0:  # (0: Hive 0.11, Decimal128 at the forced scale)
             got = c.data.reshape(-1, 2)[oi]
             assert np.array_equal(got[:, 1], words[ti, 0]) and np.array_equal(got[:, 0], words[ti, 1]), \
                 "%s col %d (decimal128) differs" % (where, tid)

@@ -76,6 +76,31 @@ def main():
         "secondary": bytes(arrays(body, "buffer2")[0]).hex(), "precision": 38, "scale": 37,
         "expected": skip_vals + [big, -big, nines, -nines],
     })
+    # Hive 0.11 decimals (precision 0, DecimalHive11ColumnReader): `scale` is
+    # the forced scale the test's mock returns; "error" = the ParseError the
+    # test expects (throwOnHive11DecimalOverflow true)
+    hive = [
+        ("testDecimalHive11", 6, "buffer1", None, list(range(-32, 33)), None),
+        ("testDecimalHive11Skip", 3, "presentBuffer", "numBuffer", skip_vals + [big, -big, nines, -nines], None),
+        ("testDecimalHive11ScaleUp", 20, "presentBuffer", "numBuffer", [10 ** i for i in range(21)], None),
+        ("testDecimalHive11ScaleDown", 0, "presentBuffer", "numBuffer", [10 ** (20 - i) for i in range(21)], None),
+        ("testDecimalHive11OverflowException", 6, "presentBuffer", "numBuffer", [0],
+         "Hive 0.11 decimal was more than 38 digits."),
+        ("testDecimalHive11OverflowExceptionNull", 6, "presentBuffer", "numBuffer", [0],
+         "Hive 0.11 decimal was more than 38 digits."),
+    ]
+    for name, forced, pres, num, expected, err in hive:
+        line, body = blk(name)
+        fx = {
+            "name": name, "source": "c++/test/TestColumnReader.cc:%d" % line, "kind": "decimal",
+            "present": bytes(arrays(body, pres)[0]).hex(),
+            "data": bytes(arrays(body, num)[0] if num else loop_num_buffer()).hex(),
+            "secondary": bytes(arrays(body, "scaleBuffer")[0]).hex(), "precision": 0, "scale": forced,
+            "expected": expected,
+        }
+        if err:
+            fx["error"] = err
+        out.append(fx)
     line, body = blk("testTimestamp", "TestColumnReader")
     dates = re.findall(r'"(\w{3} \w{3} [ \d]\d \d\d:\d\d:\d\d \d{4})\\n"', body)
     secs = [calendar.timegm(time.strptime(d, "%a %b %d %H:%M:%S %Y")) for d in dates]

@@ -51,7 +51,7 @@ def _device_decimal(data, scales, n, precision, scale):
     ctx = orc_amd.default_context(0)
     d_src = torch.frombuffer(bytearray(data) or bytearray(1), dtype=torch.uint8).cuda()
     d_sc = torch.from_numpy(np.ascontiguousarray(scales, dtype=np.int64)).cuda()
-    out = torch.zeros((n, 2) if precision > 18 else n, dtype=torch.int64, device="cuda")
+    out = torch.zeros((n, 2) if precision > 18 or precision == 0 else n, dtype=torch.int64, device="cuda")
     orc_amd.decimal_decode_device(ctx, d_src, d_sc, n, precision, scale, out, src_len=len(data))
     return out.cpu().numpy()
 
@@ -67,8 +67,12 @@ def test_decimal_timestamp_kat_on_device(fx):
     data = bytes.fromhex(fx["data"])
     if fx["kind"] == "decimal":
         scales = orc_amd.rlev1_decode(sec, n, True)
+        if fx.get("error"):  # Hive 0.11 overflow (throwOnHive11DecimalOverflow)
+            with pytest.raises(orc_amd.ParseError, match=fx["error"]):
+                _device_decimal(data, scales, n, fx["precision"], fx["scale"])
+            return
         got = _device_decimal(data, scales, n, fx["precision"], fx["scale"])
-        vals = _to_int128(got) if fx["precision"] > 18 else [int(v) for v in got]
+        vals = _to_int128(got) if fx["precision"] > 18 or fx["precision"] == 0 else [int(v) for v in got]
         assert vals == fx["expected"]
     else:
         secs = torch.from_numpy(orc_amd.rlev1_decode(data, n, True)).cuda()
@@ -98,6 +102,32 @@ def test_random_decimals_vs_oracle(precision, seed):
     want = oracle.decimal_decode(data, scales, n, col_scale, precision > 18)
     got = _device_decimal(data, scales, n, precision, col_scale)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_random_hive11_decimals_vs_oracle(seed):
+    """Hive 0.11 decimals (precision 0) at forced scales: values up to 38
+    digits rescaled up and down, against the oracle; then one value past
+    10^38 - 1 and one varint past 128 bits raise the reference's error."""
+    import orc_amd
+
+    rng = np.random.default_rng(seed)
+    n = 50_001
+    forced = int(rng.integers(0, 12))
+    scales = rng.integers(0, 24, size=n).astype(np.int64)
+    vals = []
+    for s in scales:
+        # keep |v| * 10^(forced - s) within 38 digits
+        digits = int(rng.integers(0, 39 - max(0, forced - int(s))))
+        m = int(rng.integers(0, 10 ** min(digits, 18))) * 10 ** max(0, digits - 18)
+        vals.append(-m if rng.random() < 0.5 else m)
+    data = _zz_varints(vals)
+    want = oracle.decimal_decode(data, scales, n, forced, 2)
+    np.testing.assert_array_equal(_device_decimal(data, scales, n, 0, forced), want)
+    with pytest.raises(orc_amd.ParseError, match="Hive 0.11 decimal was more than 38 digits"):
+        _device_decimal(_zz_varints([1, 10 ** 38, 2]), [0, 0, 0], 3, 0, 0)
+    with pytest.raises(orc_amd.ParseError, match="Hive 0.11 decimal was more than 38 digits"):
+        _device_decimal(_zz_varints([5]) + bytes([0x80] * 19 + [0x01]), [0, 0], 2, 0, 0)
 
 
 def test_decimal_errors_match_reference():

@@ -45,7 +45,7 @@ def test_file_matches_pyarrow(ctx, name):
 
 
 @pytest.mark.parametrize("name", ["TestOrcFile.test1.orc", "nulls-at-end-snappy.orc", "orc_index_int_string.orc",
-                                  "TestStringDictionary.testRowIndex.orc"])
+                                  "TestStringDictionary.testRowIndex.orc", "orc-file-11-format.orc"])
 def test_file_matches_reference_expected_output(ctx, name):
     want = expected_json(name)
     r, fields, got = _read_all(ctx, name)
