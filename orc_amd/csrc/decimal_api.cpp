@@ -12,7 +12,7 @@ int orcg_decimal_decode_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_l
   if (!c || (src_len && !d_src) || (nvalues && (!d_scales || !d_out)) || precision > 38)
     return ORCG_INVALID_ARGUMENT;
   (void)hipSetDevice(c->device);
-  const uint64_t ntiles_max = src_len / 16384 + 2;
+  const uint64_t ntiles_max = src_len / kVarintTile + 2;
   void *d_counts, *d_base;
   int rc = scratch(c, 5, ntiles_max * sizeof(int64_t), &d_counts);
   if (!rc) rc = scratch(c, 6, (ntiles_max + 1) * sizeof(int64_t), &d_base);

@@ -9,11 +9,15 @@
 // Decimal128 loops in steps of 10^18 (scaleInt128 :1439-1456).
 //
 // Varints have no headers to walk, so the stream is cut anywhere: the grid
-// covers it in 16 KB tiles; pass 1 counts terminator bytes (< 0x80) per tile,
+// covers it in 4 KB tiles; pass 1 counts terminator bytes (< 0x80) per tile,
 // an exclusive scan gives every tile its first value index, pass 2 stages the
-// tile (plus 64 bytes of look-back) in LDS, every thread decodes the varints
-// that END in its 64 bytes (a varint that starts in a neighbour's bytes is
-// assembled from the look-back), rescales and stores them at their index.
+// tile (plus 64 bytes of look-back) in LDS, every thread assembles the
+// varints that END in its 16 bytes (a varint that starts in a neighbour's
+// bytes is assembled from the look-back) into an LDS value stage at their
+// rank in the tile, then the workgroup rescales the staged values with
+// their scales and stores them, both coalesced (a thread's own values are
+// consecutive indices: loading their scales and storing them per thread
+// serialised one global load per varint and scattered the stores).
 //
 // TimestampColumnReader::next (:308-349): seconds (signed RLE) + the writer
 // time zone's epoch, nanos (unsigned RLE) with the trailing-zero code in the
@@ -24,8 +28,8 @@ namespace orcg {
 namespace {
 
 constexpr int kVThreads = 256;
-constexpr uint32_t kVTile = 16384;
-constexpr uint32_t kVPer = kVTile / kVThreads;  // 64 bytes per thread
+constexpr uint32_t kVTile = (uint32_t)kVarintTile;
+constexpr uint32_t kVPer = kVTile / kVThreads;  // 16 bytes per thread
 constexpr uint32_t kLook = 64;                 // look-back bytes staged before the tile
 
 __device__ const int64_t kPow10[19] = {1LL,
@@ -129,6 +133,10 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
     unsigned long long* err) {
   __shared__ uint32_t s_buf[(kLook + kVTile) / 4 + 1];
   __shared__ uint32_t s_wsum[kVThreads / 64];
+  // the tile's varints, by rank: unscaled values (Decimal64: zigzag-decoded
+  // int64; Decimal128: the raw 128-bit varint, unzigzagged in pass 2)
+  __shared__ uint64_t s_lo[kVTile];
+  __shared__ uint64_t s_hi[kMode == 0 ? 1 : kVTile];
   const uint64_t t0 = (uint64_t)blockIdx.x * kVTile;
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // stage [t0 - kLook, t0 + kVTile) (zero past the stream; bytes before 0 are
@@ -150,17 +158,17 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
   __syncthreads();
   const uint32_t r0 = kLook + (uint32_t)tid * kVPer;  // my bytes in s_buf
   uint32_t mine[kVPer / 4];
-  uint64_t tmask = 0;
+  uint32_t tmask = 0;
 #pragma unroll
   for (int i = 0; i < (int)kVPer / 4; ++i) {
     mine[i] = s_buf[r0 / 4 + i];
-    tmask |= (uint64_t)term_bits(mine[i]) << (4 * i);
+    tmask |= term_bits(mine[i]) << (4 * i);
   }
   // bytes past the end of the stream are not terminators
   const uint64_t my0 = t0 + (uint64_t)tid * kVPer;
-  if (my0 + kVPer > len) tmask &= my0 >= len ? 0ull : ((1ull << (len - my0)) - 1);
-  const uint32_t cnt = __builtin_popcountll(tmask);
-  // index of my first varint: tile base + exclusive scan of the counts
+  if (my0 + kVPer > len) tmask &= my0 >= len ? 0u : ((1u << (len - my0)) - 1u);
+  const uint32_t cnt = __builtin_popcount(tmask);
+  // rank of my first varint in the tile: exclusive scan of the counts
   uint32_t incl = cnt;
   for (int m = 1; m < 64; m <<= 1) {
     const uint32_t y = (uint32_t)__shfl_up((int)incl, m);
@@ -168,109 +176,123 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
   }
   if (lane == 63) s_wsum[wave] = incl;
   __syncthreads();
-  uint64_t k = (uint64_t)tile_base[blockIdx.x] + (incl - cnt);
-  for (int w = 0; w < wave; ++w) k += s_wsum[w];
-  if (!cnt || k >= nvalues) return;
+  const uint64_t kt = (uint64_t)tile_base[blockIdx.x];  // value index of the tile's first varint
+  uint32_t rk = incl - cnt;
+  for (int w = 0; w < wave; ++w) rk += s_wsum[w];
+  const uint32_t tile_cnt = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
 
-  // the varint ending at my first terminator starts after the previous
-  // terminator: look back (staged bytes first, then global memory)
-  uint64_t acc_lo = 0, acc_hi = 0;
-  uint32_t shift = 0;
-  bool too_long = false;  // kMode 2: more than 128 bits (:1600)
-  auto push = [&](uint32_t b) {
-    const uint64_t x = b & 0x7fu;
-    if constexpr (kMode == 2) too_long = too_long || shift > 128 || (shift == 126 && x > 3);
-    if constexpr (kMode == 0) {
-      acc_lo |= x << (shift & 63u);  // x86 shift-count masking of readInt64's UB shift
-    } else {
-      if (shift < 64) {
-        acc_lo |= x << shift;
-        if (shift > 57) acc_hi |= x >> (64 - shift);
-      } else if (shift < 128) {
-        acc_hi |= x << (shift - 64);
-      }
-    }
-    shift += 7;
-  };
-  {
-    // first byte of the varint: scan back over continuation bytes
-    int64_t s = (int64_t)my0 - 1;
-    uint32_t back = 0;
-    for (;;) {
-      if (s < 0) break;
-      uint32_t b;
-      const int64_t rel = s - ((int64_t)t0 - (int64_t)kLook);
-      if (rel >= 0) b = (s_buf[rel >> 2] >> ((rel & 3) * 8)) & 0xffu;
-      else b = src[s];
-      if (b < 0x80u) break;
-      --s;
-      ++back;
-    }
-    for (uint64_t q = (uint64_t)(s + 1); q < my0; ++q) {
-      const int64_t rel = (int64_t)q - ((int64_t)t0 - (int64_t)kLook);
-      const uint32_t b = rel >= 0 ? (s_buf[rel >> 2] >> ((rel & 3) * 8)) & 0xffu : src[q];
-      push(b);
-    }
-    (void)back;
-  }
-#pragma unroll
-  for (int i = 0; i < (int)kVPer; ++i) {
-    const uint32_t b = (mine[i >> 2] >> ((i & 3) * 8)) & 0xffu;
-    push(b);
-    if ((tmask >> i) & 1ull) {
-      if (k < nvalues) {
-        const int32_t cur = (int32_t)scales[k];
-        if constexpr (kMode == 0) {
-          int64_t v = (int64_t)((acc_lo >> 1) ^ (0 - (acc_lo & 1)));
-          if (col_scale > cur && (uint64_t)(uint32_t)(col_scale - cur) <= 18) {
-            v = (int64_t)((uint64_t)v * (uint64_t)kPow10[col_scale - cur]);
-          } else if (col_scale < cur && (uint64_t)(uint32_t)(cur - col_scale) <= 18) {
-            v /= kPow10[cur - col_scale];
-          } else if (col_scale != cur) {
-            atomicMin(err, (unsigned long long)((k << 8) | kErrDecimalScale));
-          }
-          ((int64_t*)out)[k] = v;
-        } else {
-          // unZigZagInt128 (:1291-1298): logical >> 1, negate and - 1 if odd
-          const bool odd = acc_lo & 1;
-          U128 v{(acc_lo >> 1) | (acc_hi << 63), acc_hi >> 1};
-          if (odd) {
-            v = neg128(v);
-            const uint64_t lo = v.lo - 1;
-            v.hi -= (v.lo == 0) ? 1 : 0;
-            v.lo = lo;
-          }
-          // scaleInt128 (:1439-1456) with unsigned scales
-          uint32_t s = (uint32_t)col_scale, c = (uint32_t)cur;
-          if (s > c) {
-            while (s > c && (v.lo | v.hi)) {
-              const uint32_t a = min(18u, s - c);
-              v = mul128_u64(v, (uint64_t)kPow10[a]);
-              c += a;
-            }
-          } else {
-            while (c > s && (v.lo | v.hi)) {
-              const uint32_t a = min(18u, c - s);
-              v = div128_pow10(v, a);
-              c -= a;
-            }
-          }
-          if constexpr (kMode == 2) {
-            // value >= MIN_VALUE && value <= MAX_VALUE, |v| <= 10^38 - 1 (:1616)
-            const U128 m = (int64_t)v.hi < 0 ? neg128(v) : v;
-            const uint64_t kHi = 0x4B3B4CA85A86C47Aull, kLo = 0x098A223FFFFFFFFFull;
-            const bool big = m.hi > kHi || (m.hi == kHi && m.lo > kLo);
-            if (too_long || big) atomicMin(err, (unsigned long long)((k << 8) | kErrHive11Overflow));
-          }
-          int64_t* o = (int64_t*)out + 2 * k;
-          o[0] = (int64_t)v.hi;
-          o[1] = (int64_t)v.lo;
+  // pass 1: assemble my varints into the stage
+  if (cnt && kt + rk < nvalues) {
+    uint64_t acc_lo = 0, acc_hi = 0;
+    uint32_t shift = 0;
+    bool too_long = false;  // kMode 2: more than 128 bits (:1600)
+    auto push = [&](uint32_t b) {
+      const uint64_t x = b & 0x7fu;
+      if constexpr (kMode == 2) too_long = too_long || shift > 128 || (shift == 126 && x > 3);
+      if constexpr (kMode == 0) {
+        acc_lo |= x << (shift & 63u);  // x86 shift-count masking of readInt64's UB shift
+      } else {
+        if (shift < 64) {
+          acc_lo |= x << shift;
+          if (shift > 57) acc_hi |= x >> (64 - shift);
+        } else if (shift < 128) {
+          acc_hi |= x << (shift - 64);
         }
       }
-      ++k;
-      acc_lo = acc_hi = 0;
-      shift = 0;
-      too_long = false;
+      shift += 7;
+    };
+    {
+      // first byte of the varint: scan back over continuation bytes
+      int64_t s = (int64_t)my0 - 1;
+      for (;;) {
+        if (s < 0) break;
+        uint32_t b;
+        const int64_t rel = s - ((int64_t)t0 - (int64_t)kLook);
+        if (rel >= 0) b = (s_buf[rel >> 2] >> ((rel & 3) * 8)) & 0xffu;
+        else b = src[s];
+        if (b < 0x80u) break;
+        --s;
+      }
+      for (uint64_t q = (uint64_t)(s + 1); q < my0; ++q) {
+        const int64_t rel = (int64_t)q - ((int64_t)t0 - (int64_t)kLook);
+        const uint32_t b = rel >= 0 ? (s_buf[rel >> 2] >> ((rel & 3) * 8)) & 0xffu : src[q];
+        push(b);
+      }
+    }
+    uint32_t r = rk;
+#pragma unroll
+    for (int i = 0; i < (int)kVPer; ++i) {
+      const uint32_t b = (mine[i >> 2] >> ((i & 3) * 8)) & 0xffu;
+      push(b);
+      if ((tmask >> i) & 1u) {
+        if constexpr (kMode == 0) {
+          s_lo[r] = (acc_lo >> 1) ^ (0 - (acc_lo & 1));
+        } else {
+          s_lo[r] = acc_lo;
+          s_hi[r] = acc_hi;
+          if constexpr (kMode == 2)
+            if (too_long && kt + r < nvalues) atomicMin(err, (unsigned long long)(((kt + r) << 8) | kErrHive11Overflow));
+        }
+        ++r;
+        acc_lo = acc_hi = 0;
+        shift = 0;
+        too_long = false;
+      }
+    }
+  }
+  __syncthreads();
+
+  // pass 2: rescale the staged values with their scales; loads and stores coalesced
+  const uint32_t lim = kt >= nvalues ? 0u : (uint32_t)min((uint64_t)tile_cnt, nvalues - kt);
+  for (uint32_t i = (uint32_t)tid; i < lim; i += kVThreads) {
+    const uint64_t k = kt + i;
+    const int32_t cur = (int32_t)scales[k];
+    if constexpr (kMode == 0) {
+      int64_t v = (int64_t)s_lo[i];
+      if (col_scale > cur && (uint64_t)(uint32_t)(col_scale - cur) <= 18) {
+        v = (int64_t)((uint64_t)v * (uint64_t)kPow10[col_scale - cur]);
+      } else if (col_scale < cur && (uint64_t)(uint32_t)(cur - col_scale) <= 18) {
+        v /= kPow10[cur - col_scale];
+      } else if (col_scale != cur) {
+        atomicMin(err, (unsigned long long)((k << 8) | kErrDecimalScale));
+      }
+      ((int64_t*)out)[k] = v;
+    } else {
+      const uint64_t acc_lo = s_lo[i], acc_hi = s_hi[i];
+      // unZigZagInt128 (:1291-1298): logical >> 1, negate and - 1 if odd
+      const bool odd = acc_lo & 1;
+      U128 v{(acc_lo >> 1) | (acc_hi << 63), acc_hi >> 1};
+      if (odd) {
+        v = neg128(v);
+        const uint64_t lo = v.lo - 1;
+        v.hi -= (v.lo == 0) ? 1 : 0;
+        v.lo = lo;
+      }
+      // scaleInt128 (:1439-1456) with unsigned scales
+      uint32_t s = (uint32_t)col_scale, c = (uint32_t)cur;
+      if (s > c) {
+        while (s > c && (v.lo | v.hi)) {
+          const uint32_t a = min(18u, s - c);
+          v = mul128_u64(v, (uint64_t)kPow10[a]);
+          c += a;
+        }
+      } else {
+        while (c > s && (v.lo | v.hi)) {
+          const uint32_t a = min(18u, c - s);
+          v = div128_pow10(v, a);
+          c -= a;
+        }
+      }
+      if constexpr (kMode == 2) {
+        // value >= MIN_VALUE && value <= MAX_VALUE, |v| <= 10^38 - 1 (:1616)
+        const U128 m = (int64_t)v.hi < 0 ? neg128(v) : v;
+        const uint64_t kHi = 0x4B3B4CA85A86C47Aull, kLo = 0x098A223FFFFFFFFFull;
+        if (m.hi > kHi || (m.hi == kHi && m.lo > kLo))
+          atomicMin(err, (unsigned long long)((k << 8) | kErrHive11Overflow));
+      }
+      int64_t* o = (int64_t*)out + 2 * k;
+      o[0] = (int64_t)v.hi;
+      o[1] = (int64_t)v.lo;
     }
   }
 }

@@ -118,10 +118,11 @@ int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, 
 int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t* d_nn, uint64_t n,
                        const int64_t* d_offsets, uint64_t dict_size, int64_t* d_start, int64_t* d_len);
 
-// Varint decimals (decimal_kernels.hip): per-16-KB-tile terminator counts,
+// Varint decimals (decimal_kernels.hip): per-tile (kVarintTile bytes) terminator counts,
 // then (after an exclusive scan of the counts) the decode + rescale into
 // int64 (Decimal64) or [hi, lo] int64 pairs (Decimal128, orc::Int128 layout).
 int launch_varint_tile_counts(Ctx* ctx, const uint8_t* d_src, uint64_t len, int64_t* d_counts, uint64_t* ntiles);
+constexpr uint64_t kVarintTile = 4096;
 int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
                           const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out);  // mode: 0 Decimal64, 1 Decimal128, 2 Hive 0.11
 // TimestampColumnReader value construction, in place.

@@ -615,8 +615,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       const StreamBuf& sb = c.s[kSlotData];
       const uint8_t* d_src = D->d_stage + sb.host_off;
       uint64_t ntiles = 0;
-      ORCG_ALLOC(int64_t, counts, sb.len / 16384 + 2);
-      ORCG_ALLOC(int64_t, base, sb.len / 16384 + 3);
+      ORCG_ALLOC(int64_t, counts, sb.len / kVarintTile + 2);
+      ORCG_ALLOC(int64_t, base, sb.len / kVarintTile + 3);
       if ((rc = launch_varint_tile_counts(ctx, d_src, sb.len, counts, &ntiles))) return fail_ctx(rc);
       if ((rc = launch_exclusive_scan(ctx, counts, ntiles, base))) return fail_ctx(rc);
       const uint64_t* total = defer(base + ntiles, 1);
