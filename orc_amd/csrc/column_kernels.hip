@@ -403,6 +403,12 @@ int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_
   if (n == 0) {
     return hip_check(ctx, hipMemsetAsync(d_out, 0, sizeof(int64_t), ctx->stream), "scan memset");
   }
+  if (n <= 8192) {
+    // short inputs (varint tile counts, dictionary lengths): one workgroup,
+    // one launch instead of three
+    hipLaunchKernelGGL(scan64_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const uint64_t*)d_in, n, (uint64_t*)d_out);
+    return hip_check(ctx, hipGetLastError(), "scan launch");
+  }
   const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
   if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many values");
   void* d_sums;
