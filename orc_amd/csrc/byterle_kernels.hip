@@ -9,8 +9,11 @@
 //
 // One wavefront per segment (run-aligned byte offset + index of its first
 // decoded byte). The wave walks the control bytes with wave-uniform scalar
-// arithmetic out of a 256-byte header slice held one dword per lane; runs
-// (<= 130 bytes) and literals (<= 128 bytes) are expanded by all 64 lanes.
+// arithmetic out of a 256-byte slice held one dword per lane, kept covering
+// the whole next group (control byte + up to 128 literal bytes): runs (<= 130
+// bytes) and literals (<= 128 bytes) are expanded by all 64 lanes, literal
+// bytes gathered from the slice with ds_bpermute (no memory round trip per
+// group).
 // In boolean mode every decoded byte becomes 8 output rows (chars 0/1).
 #include "rlev2_device.hh"
 
@@ -20,8 +23,9 @@ using namespace dev;
 
 struct GWin {  // 256 stream bytes at `base` (descriptor-relative), one dword per lane
   uint32_t word = 0, base = 0xffffffffu;
-  __device__ __forceinline__ void cover(__amdgpu_buffer_rsrc_t rs, uint32_t rel, int lane) {
-    if (base == 0xffffffffu || rel < base || rel + 4 > base + 256) {
+  // make [rel, rel + need) resident (need <= 252)
+  __device__ __forceinline__ void cover(__amdgpu_buffer_rsrc_t rs, uint32_t rel, int lane, uint32_t need = 4) {
+    if (base == 0xffffffffu || rel < base || rel + need > base + 256) {
       base = rel & ~3u;
       word = __builtin_amdgcn_raw_buffer_load_b32(rs, base + 4u * lane, 0, 0);
     }
@@ -88,12 +92,11 @@ __global__ __launch_bounds__(kWave) void byterle_kernel(const uint8_t* __restric
   uint64_t pos = seg_start;
   while (pos < seg_end && vi * scale < end) {
     const uint32_t rel = (uint32_t)(pos - bias);
-    w.cover(rs, rel, lane);
+    w.cover(rs, rel, lane, 132);
     const uint32_t h = w.byte(rel);
     if (h < 0x80) {  // run of h + 3 copies (readHeader, ByteRLE.cc:378-388)
       const uint32_t L = h + 3;
       if (pos + 2 > src_len) { if (lane == 0) report(err, vi, kErrByteBadRead); return; }
-      w.cover(rs, rel + 1, lane);
       const uint32_t b = w.byte(rel + 1);
       for (uint32_t j = lane; j < L; j += kWave) emit<kBool>(dst, vi + j, b, begin, end);
       pos += 2;
@@ -101,10 +104,12 @@ __global__ __launch_bounds__(kWave) void byterle_kernel(const uint8_t* __restric
     } else {  // literal group of 256 - h bytes
       const uint32_t L = 256 - h;
       if (pos + 1 + L > src_len) { if (lane == 0) report(err, vi, kErrByteBadRead); return; }
-      for (uint32_t j = lane; j < L; j += kWave) {
-        const uint32_t br = rel + 1 + j;
-        const uint32_t wd = __builtin_amdgcn_raw_buffer_load_b32(rs, br & ~3u, 0, 0);
-        emit<kBool>(dst, vi + j, (wd >> ((br & 3u) * 8)) & 0xffu, begin, end);
+      for (uint32_t j0 = 0; j0 < L; j0 += kWave) {
+        // every lane takes part in the gather (a wave-uniform loop)
+        const uint32_t j = j0 + (uint32_t)lane;
+        const uint32_t o = rel + 1 + j - w.base;
+        const uint32_t wd = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((o >> 2) & 63u) * 4, (int)w.word);
+        if (j < L) emit<kBool>(dst, vi + j, (wd >> ((o & 3u) * 8)) & 0xffu, begin, end);
       }
       pos += 1 + L;
       vi += L;

@@ -79,32 +79,49 @@ __global__ __launch_bounds__(1024) void scan_kernel(const uint32_t* __restrict__
   if (threadIdx.x == 0) offsets[n] = carry_s;
 }
 
+// One workgroup per kTile rows; row r = tile + 256 k + tid (k < 16), so the
+// not-null bytes, the dense values (consecutive ranks) and the output rows
+// are all read and written coalesced. A row's rank: the tile's first rank +
+// the non-null rows of the earlier 256-row chunks + those of the lower waves
+// of its chunk + a ballot popcount inside its wave.
 template <typename T, bool kFill>
 __global__ __launch_bounds__(kThreads) void scatter_kernel(const T* __restrict__ dense, const uint8_t* __restrict__ nn,
                                                             uint64_t n, const uint64_t* __restrict__ tile_off,
                                                             T* __restrict__ out, T fill) {
-  __shared__ uint32_t wsum[kThreads / kWave];
+  constexpr int kChunks = kTile / kThreads;
+  static_assert(kChunks * kThreads == kTile, "tile = whole 256-row chunks");
+  __shared__ uint32_t s_cnt[kChunks][kThreads / kWave];
   const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
-  const uint64_t row0 = (uint64_t)blockIdx.x * kTile + threadIdx.x * 16u;
-  const u4 v = row0 < n ? load16(nn, row0, n) : u4{0, 0, 0, 0};
-  const uint32_t c = nn_bytes_count(v);
-  uint32_t inc = c;
-  for (int d = 1; d < kWave; d <<= 1) {
-    const uint32_t y = __shfl_up(inc, d, kWave);
-    if (lane >= d) inc += y;
-  }
-  if (lane == kWave - 1) wsum[wv] = inc;
-  __syncthreads();
-  uint32_t before = 0;
-  for (int w = 0; w < wv; ++w) before += wsum[w];
-  uint64_t rank = tile_off[blockIdx.x] + before + inc - c;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTile;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t flags = 0;  // bit k: my row of chunk k is not null
+  uint32_t below_cnt[kChunks];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint64_t r = row0 + k;
+  for (int k = 0; k < kChunks; ++k) {
+    const uint64_t r = t0 + (uint64_t)k * kThreads + threadIdx.x;
+    const bool f = r < n && nn[r] != 0;
+    const uint64_t b = __ballot(f);
+    flags |= (f ? 1u : 0u) << k;
+    below_cnt[k] = (uint32_t)__builtin_popcountll(b & below);
+    if (lane == 0) s_cnt[k][wv] = (uint32_t)__builtin_popcountll(b);
+  }
+  __syncthreads();
+  uint64_t base = tile_off[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kChunks; ++k) {
+    const uint64_t r = t0 + (uint64_t)k * kThreads + threadIdx.x;
+    uint32_t lower = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / kWave; ++w) {
+      const uint32_t c = s_cnt[k][w];
+      lower += w < wv ? c : 0u;
+      all += c;
+    }
     if (r < n) {
-      if ((v[k >> 2] >> (8 * (k & 3))) & 0xffu) out[r] = dense[rank++];
+      if ((flags >> k) & 1u) out[r] = dense[base + lower + below_cnt[k]];
       else if (kFill) out[r] = fill;
     }
+    base += all;
   }
 }
 

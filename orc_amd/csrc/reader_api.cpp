@@ -1106,7 +1106,8 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   parallel_for(rle.size(), [&](size_t q) {
     StreamBuf& sb = *rle[q];
     const uint8_t* p = hs.h + sb.host_off;
-    if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, 16u << 10, 16384));
+    // byte / boolean RLE without row-index segments: 1 KB segments (one wave each: enough waves to fill the GPU)
+    if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, 1u << 10, 1024));
     else if (rle_kind[q] == 1) sb.plan.reset(make_v1_plan(p, sb.len, 16u << 10, 8192));
     else sb.plan.reset(make_plan(p, sb.len, 16u << 10, 8192));
   });
