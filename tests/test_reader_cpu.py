@@ -139,3 +139,20 @@ def test_metadata_matches_reference_testmatch(d):
     for k, v in d["metadata"].items():
         assert meta[k] == bytes.fromhex(v), k
     assert "foo" not in meta
+
+
+def test_hive11_decimal_options():
+    """RowReaderOptions::forcedScaleOnHive11Decimal (default 6, Reader.hh:258-271)
+    on a Hive 0.11 file (decimal1 has precision 0); only the throwing overflow
+    mode (the reference's default) is supported. No GPU."""
+    r = orc_amd.Reader(path("orc-file-11-format.orc"))
+    dec = [t for t in r.types if t.kind == 14]
+    assert dec and all(t.precision == 0 for t in dec)
+    assert r.hive11_scale == 6
+    r.set_hive11_decimal(3)
+    assert r.hive11_scale == 3
+    with pytest.raises(orc_amd.OrcError):
+        r.set_hive11_decimal(6, throw_on_overflow=False)
+    with pytest.raises(orc_amd.OrcError):
+        r.set_hive11_decimal(39)
+    assert r.hive11_scale == 3
