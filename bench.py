@@ -330,12 +330,18 @@ def main():
     def step():
         orc_amd.decode_positions_device(ctx, d_src, d_pos, args.stride, N, True, d_out)
 
-    # verify one decode first, then warm up: the host-side compare leaves the
-    # GPU idle for ~1 s, and the timed steps must not start from idle clocks
+    # verify one decode first (every value, compared on the device against the
+    # generated values uploaded beforehand, so no host round trip leaves the
+    # GPU idle between the check and the warm-up), then warm up
     if not args.no_verify:
+        with torch.cuda.stream(stream):
+            d_want = torch.from_numpy(values).to("cuda")
+        stream.synchronize()
         step()
+        with torch.cuda.stream(stream):
+            ok = bool(torch.equal(d_out, d_want))
         ctx.synchronize()
-        ok = torch.equal(d_out.cpu(), torch.from_numpy(values))
+        del d_want
         if not ok:
             raise SystemExit("decode mismatch on rank %d" % rank)
     for _ in range(args.warmup):

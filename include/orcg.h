@@ -206,6 +206,38 @@ int orcg_byte_rle_decoder_skip(orcg_byte_rle_decoder* dec, uint64_t n);
 int orcg_byte_rle_decoder_seek(orcg_byte_rle_decoder* dec, const uint64_t* positions, uint64_t npositions);
 const char* orcg_byte_rle_decoder_last_error(const orcg_byte_rle_decoder* dec);
 
+/* ---- Java TreeReader face (java/core/src/java/org/apache/orc/impl/
+ * TreeReaderFactory.java): the ColumnVector fields a JNI shim fills, built
+ * from the GPU-decoded streams of the stateful decoders above. Java boolean[]
+ * travels as one byte per row (1 = true). Errors: the status, and the message
+ * from orcg_java_last_error() (this thread's last failure). */
+const char* orcg_java_last_error(void);
+/* TreeReader.nextVector (TreeReaderFactory.java:405-441): `present` is the
+ * column's PRESENT stream as a boolean decoder (BitFieldReader,
+ * BitFieldReader.java:30-57; NULL = no PRESENT stream), parent_is_null the
+ * parent's isNull (NULL = none). Writes is_null[batch] and *no_nulls; with a
+ * PRESENT stream or a parent mask *is_repeating = !noNulls && every row null,
+ * otherwise *is_repeating is left unchanged (as the reference leaves it). */
+int orcg_java_tree_present_next(orcg_byte_rle_decoder* present, const uint8_t* parent_is_null, uint64_t batch,
+                                uint8_t* is_null, int* no_nulls, int* is_repeating);
+/* StringDictionaryTreeReader.nextVector's readDictionaryByteArray
+ * (TreeReaderFactory.java:2396-2478), no filter context: the DATA indices
+ * through RunLengthIntegerReaderV2.nextVector (`data`, unsigned; scratch =
+ * the reader's scratchlcv.vector, kept by the caller across batches), then
+ * BytesColumnVector.setRef(i, dictionaryBuffer, start[i], length[i]) per row:
+ * start = dictionaryOffsets[idx], length = the next offset - start, or
+ * buffer_len - start for the last array entry (getDictionaryEntryLength);
+ * null rows (0, 0); a repeating index vector sets row 0 only and returns
+ * *is_repeating = 1. is_null / *no_nulls / *is_repeating come in from
+ * orcg_java_tree_present_next (the result vector's fields). has_buffer = 0
+ * (dictionaryBuffer == null): non-null rows get the empty string, or with
+ * dict_offsets NULL too the batch becomes one repeating null. An index
+ * outside the offsets array: ORCG_PARSE_ERROR with Java's
+ * "Index i out of bounds for length n". */
+int orcg_java_dictionary_next(orcg_rle_decoder* data, const int32_t* dict_offsets, uint64_t dict_offsets_len,
+                              int has_buffer, int64_t buffer_len, uint8_t* is_null, int* no_nulls, int* is_repeating,
+                              uint64_t batch, int64_t* scratch, int32_t* start, int32_t* length);
+
 /* ---- RLEv1 (DIRECT / DICTIONARY encodings, format 0.11 files) ------------
  * Replaces RleDecoderV1 (c++/src/RLEv1.hh:51-96, RLEv1.cc:140-300) as chosen
  * by createRleDecoder for RleVersion_1 (c++/src/RLE.cc:48-60). Plans cut the

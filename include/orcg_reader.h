@@ -162,11 +162,16 @@ int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t type_id
 /* ---- RowReader (c++/include/orc/Reader.hh:640-790; c++/src/Reader.cc
  * RowReaderImpl) over the GPU stripe decode. Batches hold at most `capacity`
  * rows and never span two stripes (RowReaderImpl::next, Reader.cc:1402-1403).
- * Each batch is a row range of the stripe decoded in HBM; per column,
- * orcg_row_reader_column gives the stripe's column view plus the element
- * range [begin, begin + count) of the batch (through list / map offsets and
- * union tags), which host adapters copy out. The row reader borrows the
- * reader (and its column selection and stripe slot 0). */
+ * Each stripe is decoded in HBM and copied once into a pinned host slab owned
+ * by the row reader; a worker thread decodes stripe s + 1 (and decompresses
+ * s + 2) while the caller reads stripe s (startNextStripe's prefetch,
+ * Reader.cc:1336-1360), so next() waits only for the slab of a new stripe.
+ * Per column, orcg_row_reader_column gives the stripe's column view with
+ * HOST pointers into that slab (valid until the next orcg_row_reader_next /
+ * seek / destroy) plus the element range [begin, begin + count) of the batch
+ * (through list / map offsets and union tags). A row reader keeps its own
+ * RowReaderOptions (include, lazy decoding) and device memory; it borrows
+ * the reader (destroy row readers first), whose decodes it takes turns with. */
 typedef struct orcg_row_reader orcg_row_reader;
 typedef struct {
   uint64_t offset, length;   /* RowReaderOptions::range: stripes whose offset lies in [offset, offset + length) */
@@ -177,12 +182,17 @@ typedef struct {
 /* opts NULL = the whole file, every column */
 int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* opts, orcg_row_reader** out);
 void orcg_row_reader_destroy(orcg_row_reader* rr);
+/* 1 if the type id is read by this row reader (RowReader::getSelectedColumns) */
+int orcg_row_reader_is_selected(const orcg_row_reader* rr, uint32_t type_id);
 /* RowReader::next: *rows = rows in the new batch (0 at the end) */
 int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows);
 /* RowReader::getRowNumber: first row of the last batch (UINT64_MAX before the first) */
 uint64_t orcg_row_reader_row_number(const orcg_row_reader* rr);
+/* stripe of the last batch (UINT64_MAX before the first) */
+uint64_t orcg_row_reader_stripe(const orcg_row_reader* rr);
 /* RowReader::seekToRow: the next batch starts at `row` */
 int orcg_row_reader_seek_to_row(orcg_row_reader* rr, uint64_t row);
+/* the last batch's view of column type_id (host pointers, see above) */
 int orcg_row_reader_column(const orcg_row_reader* rr, uint32_t type_id, orcg_column_view* view, uint64_t* begin,
                            uint64_t* count);
 

@@ -27,6 +27,8 @@ from .rle import (  # noqa: F401
     default_context,
     encode_direct,
     encode_runs,
+    java_dictionary_next,
+    java_tree_present_next,
     rlev1_decode,
     rlev2_decode,
     rlev2_variants,

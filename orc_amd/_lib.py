@@ -97,6 +97,10 @@ SIGNATURES = [
     ("orcg_decimal_decode_device", [vp, vp, u64, vp, u64, ctypes.c_uint32, i32, vp], i32),
     ("orcg_timestamp_decode_device", [vp, vp, vp, u64, ctypes.c_int64], i32),
     ("orcg_decode_integer_column", [vp, vp, u64, vp, u64, i32, u64, vp, vp], i32),
+    ("orcg_java_last_error", [], cp),
+    ("orcg_java_tree_present_next", [vp, vp, u64, vp, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
+    ("orcg_java_dictionary_next", [vp, vp, u64, i32, ctypes.c_int64, vp, ctypes.POINTER(i32), ctypes.POINTER(i32),
+                                   u64, vp, vp, vp], i32),
     ("orcg_rlev2_encode_direct", [vp, u64, i32, i32, vp, u64, ctypes.POINTER(u64), u64, vp], i32),
     ("orcg_rlev2_encode_runs", [vp, u64, i32, vp, vp, u64, vp, u64, ctypes.POINTER(u64), vp], i32),
 ]
@@ -173,6 +177,8 @@ SIGNATURES += [
     ("orcg_row_reader_create", [vp, ctypes.POINTER(RowReaderOptions), ctypes.POINTER(vp)], i32),
     ("orcg_row_reader_destroy", [vp], None),
     ("orcg_row_reader_next", [vp, u64, ctypes.POINTER(u64)], i32),
+    ("orcg_row_reader_is_selected", [vp, u32], i32),
+    ("orcg_row_reader_stripe", [vp], u64),
     ("orcg_row_reader_row_number", [vp], u64),
     ("orcg_row_reader_seek_to_row", [vp, u64], i32),
     ("orcg_row_reader_column", [vp, u32, ctypes.POINTER(ColumnView), ctypes.POINTER(u64), ctypes.POINTER(u64)],

@@ -17,7 +17,7 @@ OUT = os.path.join(HERE, "liborcgpu_prof.so" if PROF else ("liborcgpu_ab.so" if 
 OBJ = os.path.join(HERE, "build_prof" if PROF else ("build_ab" if AB else "build"))
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "decimal_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "decimal_api.cpp", "encoder.cpp"]
+SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "decimal_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "decimal_api.cpp", "encoder.cpp", "java_face.cpp"]
 if PROF or AB:
     SOURCES.append("probe_kernels.hip")
 HEADERS = ["orcg_internal.hh", "rlev2_device.hh", "orc_file.hh", os.path.join("..", "..", "include", "orcg.h"),
@@ -40,7 +40,7 @@ def _mtime(p):
 def build(force=False, verbose=False):
     os.makedirs(OBJ, exist_ok=True)
     hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
-    objs = []
+    objs, cmds = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OBJ, s + ".o")
@@ -52,9 +52,20 @@ def build(force=False, verbose=False):
             cmd[1:1] = ["-x", "hip", "--offload-arch=" + ARCH]
         else:
             cmd[1:1] = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+        cmds.append(cmd)
+    # translation units compile in parallel (the slowest, rlev2_tiled.hip, first)
+    cmds.sort(key=lambda c: "rlev2_tiled" not in c[-3])
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)
+
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "8") or 8), os.cpu_count() or 1))
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(run, c) for c in cmds]:
+            f.result()
     if force or _mtime(OUT) < max(_mtime(o) for o in objs):
         cmd = [HIPCC, "-shared", "-fPIC", "-o", OUT] + objs + ["-Wl,-soname," + os.path.basename(OUT), "-lz", "-ldl", "-lpthread"]
         if verbose:

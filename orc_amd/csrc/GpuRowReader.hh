@@ -33,7 +33,9 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <functional>
 #include <list>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -63,9 +65,28 @@ struct LongVectorBatch : ColumnVectorBatch {
   using ColumnVectorBatch::ColumnVectorBatch;
   std::vector<int64_t> data;
 };
+// RowReaderOptions::setUseTightNumericVector batches (Vector.hh IntegerVectorBatch<T>,
+// FloatingVectorBatch<float>): BOOLEAN / BYTE -> Byte, SHORT -> Short, INT ->
+// Int, FLOAT -> Float (ColumnReader.cc:1703-1790)
+struct IntVectorBatch : ColumnVectorBatch {
+  using ColumnVectorBatch::ColumnVectorBatch;
+  std::vector<int32_t> data;
+};
+struct ShortVectorBatch : ColumnVectorBatch {
+  using ColumnVectorBatch::ColumnVectorBatch;
+  std::vector<int16_t> data;
+};
+struct ByteVectorBatch : ColumnVectorBatch {
+  using ColumnVectorBatch::ColumnVectorBatch;
+  std::vector<int8_t> data;
+};
 struct DoubleVectorBatch : ColumnVectorBatch {
   using ColumnVectorBatch::ColumnVectorBatch;
   std::vector<double> data;
+};
+struct FloatVectorBatch : ColumnVectorBatch {
+  using ColumnVectorBatch::ColumnVectorBatch;
+  std::vector<float> data;
 };
 struct StringVectorBatch : ColumnVectorBatch {
   using ColumnVectorBatch::ColumnVectorBatch;
@@ -143,6 +164,11 @@ class RowReaderOptions {
     lazy_ = on;
     return *this;
   }
+  RowReaderOptions& setUseTightNumericVector(bool on) {
+    tight_ = on;
+    return *this;
+  }
+  bool getUseTightNumericVector() const { return tight_; }
   uint64_t getOffset() const { return offset_; }
   uint64_t getLength() const { return length_; }
   bool getEnableLazyDecoding() const { return lazy_; }
@@ -154,6 +180,7 @@ class RowReaderOptions {
   bool hasInclude_ = false;
   uint64_t offset_ = 0, length_ = std::numeric_limits<uint64_t>::max();
   bool lazy_ = false;
+  bool tight_ = false;
 };
 
 class Reader;
@@ -168,12 +195,18 @@ class RowReader {
   bool next(ColumnVectorBatch& batch);
   uint64_t getRowNumber() const { return orcg_row_reader_row_number(rr_); }
   void seekToRow(uint64_t rowNumber);
+  // RowReader::getSelectedColumns()[id]
+  bool isSelected(uint32_t id) const { return orcg_row_reader_is_selected(rr_, id) != 0; }
 
  private:
   void fill(uint32_t id, ColumnVectorBatch& b);
   Reader& r_;
   orcg_row_reader* rr_ = nullptr;
   bool lazy_ = false;
+  bool tight_ = false;
+  // the current stripe's dictionaries, shared by its batches (lazy decoding)
+  uint64_t dict_stripe_ = ~0ull;
+  std::map<uint32_t, std::shared_ptr<StringDictionary>> dicts_;
 };
 
 class Reader {
@@ -254,16 +287,37 @@ class Reader {
     dst.resize(count);
     if (count) check(orcg_reader_copy_to_host(r_, dst.data(), (const T*)src + first, count * sizeof(T)));
   }
+  // row reader views point into its pinned host slab: plain copies
+  template <typename T>
+  static void hcopy(std::vector<T>& dst, const void* src, uint64_t count, uint64_t first = 0) {
+    dst.resize(count);
+    if (count) memcpy(dst.data(), (const T*)src + first, count * sizeof(T));
+  }
 
  private:
   Context& ctx_;
   orcg_reader* r_ = nullptr;
 };
 
-inline std::unique_ptr<ColumnVectorBatch> make_batch(const Reader& r, uint32_t id, uint64_t cap, bool lazy) {
+using Selected = std::function<bool(uint32_t)>;
+
+inline std::unique_ptr<ColumnVectorBatch> make_batch(const Reader& r, uint32_t id, uint64_t cap, bool lazy,
+                                                     const Selected& sel, bool tight = false) {
   const orcg_type_info t = r.getType(id);
   switch (t.kind) {
+    case ORCG_TYPE_BOOLEAN:
+    case ORCG_TYPE_BYTE:
+      if (tight) return std::make_unique<ByteVectorBatch>(t.kind, cap);
+      return std::make_unique<LongVectorBatch>(t.kind, cap);
+    case ORCG_TYPE_SHORT:
+      if (tight) return std::make_unique<ShortVectorBatch>(t.kind, cap);
+      return std::make_unique<LongVectorBatch>(t.kind, cap);
+    case ORCG_TYPE_INT:
+      if (tight) return std::make_unique<IntVectorBatch>(t.kind, cap);
+      return std::make_unique<LongVectorBatch>(t.kind, cap);
     case ORCG_TYPE_FLOAT:
+      if (tight) return std::make_unique<FloatVectorBatch>(t.kind, cap);
+      return std::make_unique<DoubleVectorBatch>(t.kind, cap);
     case ORCG_TYPE_DOUBLE: return std::make_unique<DoubleVectorBatch>(t.kind, cap);
     case ORCG_TYPE_STRING:
     case ORCG_TYPE_BINARY:
@@ -279,32 +333,34 @@ inline std::unique_ptr<ColumnVectorBatch> make_batch(const Reader& r, uint32_t i
     case ORCG_TYPE_TIMESTAMP_INSTANT: return std::make_unique<TimestampVectorBatch>(t.kind, cap);
     case ORCG_TYPE_LIST: {
       auto b = std::make_unique<ListVectorBatch>(t.kind, cap);
-      b->elements = make_batch(r, r.getSubtypes(id)[0], cap, lazy);
+      b->elements = make_batch(r, r.getSubtypes(id)[0], cap, lazy, sel, tight);
       return b;
     }
     case ORCG_TYPE_MAP: {
       auto b = std::make_unique<MapVectorBatch>(t.kind, cap);
       const auto s = r.getSubtypes(id);
-      b->keys = make_batch(r, s[0], cap, lazy);
-      b->elements = make_batch(r, s[1], cap, lazy);
+      b->keys = make_batch(r, s[0], cap, lazy, sel, tight);
+      b->elements = make_batch(r, s[1], cap, lazy, sel, tight);
       return b;
     }
     case ORCG_TYPE_STRUCT: {
       // the selected fields only (Type::createRowBatch of the selected type)
       auto b = std::make_unique<StructVectorBatch>(t.kind, cap);
-      for (uint32_t s : r.getSelectedSubtypes(id)) b->fields.push_back(make_batch(r, s, cap, lazy));
+      for (uint32_t s : r.getSubtypes(id))
+        if (sel(s)) b->fields.push_back(make_batch(r, s, cap, lazy, sel, tight));
       return b;
     }
     case ORCG_TYPE_UNION: {
       auto b = std::make_unique<UnionVectorBatch>(t.kind, cap);
-      for (uint32_t s : r.getSubtypes(id)) b->children.push_back(make_batch(r, s, cap, lazy));
+      for (uint32_t s : r.getSubtypes(id)) b->children.push_back(make_batch(r, s, cap, lazy, sel, tight));
       return b;
     }
     default: return std::make_unique<LongVectorBatch>(t.kind, cap);
   }
 }
 
-inline RowReader::RowReader(Reader& r, const RowReaderOptions& opts) : r_(r), lazy_(opts.getEnableLazyDecoding()) {
+inline RowReader::RowReader(Reader& r, const RowReaderOptions& opts)
+    : r_(r), lazy_(opts.getEnableLazyDecoding()), tight_(opts.getUseTightNumericVector()) {
   std::vector<uint8_t> inc;
   orcg_row_reader_options o;
   memset(&o, 0, sizeof(o));
@@ -324,7 +380,7 @@ inline RowReader::RowReader(Reader& r, const RowReaderOptions& opts) : r_(r), la
 }
 
 inline std::unique_ptr<ColumnVectorBatch> RowReader::createRowBatch(uint64_t capacity) const {
-  return make_batch(r_, 0, capacity, lazy_);
+  return make_batch(r_, 0, capacity, lazy_, [this](uint32_t id) { return isSelected(id); }, tight_);
 }
 
 inline bool RowReader::next(ColumnVectorBatch& batch) {
@@ -338,30 +394,57 @@ inline bool RowReader::next(ColumnVectorBatch& batch) {
 
 inline void RowReader::seekToRow(uint64_t rowNumber) { r_.check(orcg_row_reader_seek_to_row(rr_, rowNumber)); }
 
+template <typename T, typename S>
+inline void narrow_copy(std::vector<T>& dst, const void* src, uint64_t n, uint64_t first) {
+  // static_cast<T> of the decoded values, as the reference's decoders narrow
+  const S* p = (const S*)src + first;
+  dst.resize(n);
+  for (uint64_t i = 0; i < n; ++i) dst[i] = static_cast<T>(p[i]);
+}
+
 inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
   orcg_column_view v;
   uint64_t first = 0, n = 0;
   r_.check(orcg_row_reader_column(rr_, id, &v, &first, &n));
-  if (!v.decoded)  // TIMESTAMP of a non-UTC writer zone or a Hive 0.11 decimal (include/orcg_reader.h)
+  if (!v.decoded)  // TIMESTAMP of a non-UTC writer zone (include/orcg_reader.h)
     throw InvalidArgument("column " + std::to_string(id) + " is not decoded by the GPU reader");
+  // the view points into the row reader's host slab: plain copies
   b.numElements = n;
   if (n > b.capacity) b.capacity = n;  // children grow like the reference's resize()
   b.hasNulls = v.has_nulls != 0;
-  if (b.hasNulls) r_.copy(b.notNull, v.not_null, n, first);
+  if (b.hasNulls) Reader::hcopy(b.notNull, v.not_null, n, first);
   else b.notNull.assign(n, 1);
-  const std::vector<uint32_t> subs =
-      v.kind == ORCG_TYPE_STRUCT ? r_.getSelectedSubtypes(id) : r_.getSubtypes(id);
+  std::vector<uint32_t> subs;
+  for (uint32_t s : r_.getSubtypes(id))
+    if (v.kind != ORCG_TYPE_STRUCT || isSelected(s)) subs.push_back(s);
   if (auto* l = dynamic_cast<LongVectorBatch*>(&b)) {
-    r_.copy(l->data, v.data, n, first);
+    Reader::hcopy(l->data, v.data, n, first);
+  } else if (auto* i32 = dynamic_cast<IntVectorBatch*>(&b)) {
+    narrow_copy<int32_t, int64_t>(i32->data, v.data, n, first);
+  } else if (auto* i16 = dynamic_cast<ShortVectorBatch*>(&b)) {
+    narrow_copy<int16_t, int64_t>(i16->data, v.data, n, first);
+  } else if (auto* i8 = dynamic_cast<ByteVectorBatch*>(&b)) {
+    narrow_copy<int8_t, int64_t>(i8->data, v.data, n, first);
   } else if (auto* d = dynamic_cast<DoubleVectorBatch*>(&b)) {
-    r_.copy(d->data, v.data, n, first);
+    Reader::hcopy(d->data, v.data, n, first);
+  } else if (auto* f = dynamic_cast<FloatVectorBatch*>(&b)) {
+    narrow_copy<float, double>(f->data, v.data, n, first);
   } else if (auto* e = dynamic_cast<EncodedStringVectorBatch*>(&b); e && v.index) {
-    // nextEncoded: index + the stripe's dictionary (ColumnReader.cc:596-607)
+    // nextEncoded: index + the stripe's dictionary (ColumnReader.cc:596-607),
+    // one host dictionary per stripe shared by its batches
     e->isEncoded = true;
-    r_.copy(e->index, v.index, n, first);
-    auto dict = std::make_shared<StringDictionary>();
-    r_.copy(dict->dictionaryBlob, v.blob, v.blob_len);
-    r_.copy(dict->dictionaryOffset, v.dict_offsets, v.dict_size + 1);
+    Reader::hcopy(e->index, v.index, n, first);
+    const uint64_t stripe = orcg_row_reader_stripe(rr_);
+    if (stripe != dict_stripe_) {
+      dicts_.clear();
+      dict_stripe_ = stripe;
+    }
+    std::shared_ptr<StringDictionary>& dict = dicts_[id];
+    if (!dict) {
+      dict = std::make_shared<StringDictionary>();
+      Reader::hcopy(dict->dictionaryBlob, v.blob, v.blob_len);
+      Reader::hcopy(dict->dictionaryOffset, v.dict_offsets, v.dict_size + 1);
+    }
     e->dictionary = dict;
     e->data.assign(n, nullptr);
     e->length.assign(n, 0);
@@ -369,8 +452,8 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
       if (!b.hasNulls || b.notNull[i]) dict->getValueByIndex(e->index[i], e->data[i], e->length[i]);
   } else if (auto* s = dynamic_cast<StringVectorBatch*>(&b)) {
     std::vector<int64_t> start;
-    r_.copy(start, v.data, n, first);
-    r_.copy(s->length, v.length, n, first);
+    Reader::hcopy(start, v.data, n, first);
+    Reader::hcopy(s->length, v.length, n, first);
     // dictionary: the whole blob; direct: the byte span the batch covers
     uint64_t lo = 0, hi = v.blob_len;
     if (!v.index) {
@@ -383,30 +466,30 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
         }
       if (lo == ~0ull) lo = hi = 0;
     }
-    r_.copy(s->blob, v.blob, hi - lo, lo);
+    Reader::hcopy(s->blob, v.blob, hi - lo, lo);
     s->data.resize(n);
     for (uint64_t i = 0; i < n; ++i) s->data[i] = s->blob.data() + (s->length[i] > 0 ? start[i] - (int64_t)lo : 0);
   } else if (auto* d64 = dynamic_cast<Decimal64VectorBatch*>(&b)) {
     const orcg_type_info t = r_.getType(id);
     d64->precision = (int32_t)t.precision;
     d64->scale = (int32_t)t.scale;
-    r_.copy(d64->values, v.data, n, first);
+    Reader::hcopy(d64->values, v.data, n, first);
   } else if (auto* d128 = dynamic_cast<Decimal128VectorBatch*>(&b)) {
     const orcg_type_info t = r_.getType(id);
     d128->precision = (int32_t)t.precision;
     // Hive 0.11 decimals: the forced scale (DecimalHive11ColumnReader::next)
     d128->scale = t.precision == 0 ? (int32_t)orcg_reader_hive11_scale(r_.get()) : (int32_t)t.scale;
-    r_.copy(d128->values, v.data, n, first);  // [hi, lo] per value = Int128's layout
+    Reader::hcopy(d128->values, v.data, n, first);  // [hi, lo] per value = Int128's layout
   } else if (auto* ts = dynamic_cast<TimestampVectorBatch*>(&b)) {
-    r_.copy(ts->data, v.data, n, first);
-    r_.copy(ts->nanoseconds, v.secondary, n, first);
+    Reader::hcopy(ts->data, v.data, n, first);
+    Reader::hcopy(ts->nanoseconds, v.secondary, n, first);
   } else if (auto* lb = dynamic_cast<ListVectorBatch*>(&b)) {
-    r_.copy(lb->offsets, v.offsets, n + 1, first);
+    Reader::hcopy(lb->offsets, v.offsets, n + 1, first);
     const int64_t base = lb->offsets[0];
     for (auto& o : lb->offsets) o -= base;
     fill(subs[0], *lb->elements);
   } else if (auto* mb = dynamic_cast<MapVectorBatch*>(&b)) {
-    r_.copy(mb->offsets, v.offsets, n + 1, first);
+    Reader::hcopy(mb->offsets, v.offsets, n + 1, first);
     const int64_t base = mb->offsets[0];
     for (auto& o : mb->offsets) o -= base;
     fill(subs[0], *mb->keys);
@@ -414,9 +497,9 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
   } else if (auto* sb = dynamic_cast<StructVectorBatch*>(&b)) {
     for (size_t i = 0; i < subs.size(); ++i) fill(subs[i], *sb->fields[i]);
   } else if (auto* ub = dynamic_cast<UnionVectorBatch*>(&b)) {
-    r_.copy(ub->tags, v.tags, n, first);
+    Reader::hcopy(ub->tags, v.tags, n, first);
     std::vector<int64_t> offs;
-    r_.copy(offs, v.offsets, n, first);
+    Reader::hcopy(offs, v.offsets, n, first);
     // offsets relative to each child's first row in this batch
     std::vector<int64_t> base(subs.size(), -1);
     for (uint64_t i = 0; i < n; ++i)

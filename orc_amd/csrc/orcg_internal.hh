@@ -96,7 +96,7 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
 
 // RLEv2 kernel variants a context accepts (orcg_rlev2_variants): 0 default,
 // 1 wave-walk, and pins of single tiled instances (launch_rlev2_tiled).
-constexpr int kMaxRlev2Variant = 24;
+constexpr int kMaxRlev2Variant = 27;
 bool rlev2_variant_valid(int v);
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
@@ -107,6 +107,8 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
 // instance the default's density rule picks (or the pinned variant);
 // variant 1 falls back to one launch per stream.
 int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs);
+// Variants whose instances take job tables with row-index segments (RleJob::trip).
+bool rlev2_multi_capable(int variant);
 
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
                    bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst);

@@ -18,11 +18,14 @@
 #include <unistd.h>
 
 #include <atomic>
-#include <functional>
 #include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <thread>
 
 #include "../../include/orcg_reader.h"
@@ -247,6 +250,9 @@ struct DevSlot {
 };
 
 struct orcg_reader {
+  // serialises decodes: the reader's own reads and the row readers' prefetch
+  // workers share its decode state (stages, batch tables, checks)
+  std::mutex mu;
   Ctx* ctx = nullptr;
   const uint8_t* file = nullptr;
   uint64_t file_len = 0;
@@ -469,7 +475,7 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
   if (!force_v2 && (c.encoding == kDirect || c.encoding == kDictionary)) return ORCG_OK;
   if (!sb.pos && count > sb.plan->values) return ORCG_OK;
   RleJob j{};
-  if (sb.pos && cur_rows) {
+  if (sb.pos && cur_rows && rlev2_multi_capable(ctx->rlev2_variant)) {
     // the row index is the segment table (no rg_segtab launch): collect()
     // only queues columns whose rows are all values (no mask)
     j.trip = (const int64_t*)(D->d_stage + sb.rg_off);
@@ -1277,19 +1283,120 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
 // ---- RowReader: batches of at most `capacity` rows over the stripes of a
 // byte range (c++/src/Reader.cc RowReaderImpl: ctor :307-363, next
 // :1392-1442, seekToRow :428-499, getRowNumber :424-426, markEndOfFile
-// :1128-1139). The GPU decodes a whole stripe into HBM once; each batch is a
-// row range of it (per column: an element range, through list / map offsets
-// and union tags), which the host adapters copy out.
+// :1128-1139, startNextStripe's prefetch :1336-1360).
+//
+// The GPU decodes a whole stripe into HBM, which is copied once into a pinned
+// host slab; each batch is a row range of that slab (per column an element
+// range, through list / map offsets and union tags), so next() touches no
+// device and waits for nothing but the slab of a new stripe. A worker thread
+// per row reader prepares (host decompression), decodes and copies stripe
+// s + 1 (and decompresses s + 2) while the caller consumes stripe s. The
+// row reader keeps its own RowReaderOptions (include, lazy decoding), its own
+// device slot and slabs; decodes take the reader's lock.
+
+// A decoded stripe in pinned host memory.
+struct HostSlab {
+  uint64_t stripe = ~0ull;
+  uint8_t* h = nullptr;
+  size_t cap = 0;
+  std::vector<ColOut> out;  // host pointers into h
+  int rc = ORCG_OK;
+  std::string err;
+  ~HostSlab() {
+    if (h) (void)hipHostFree(h);
+  }
+};
+
+// The buffers of a decoded column, in the batch layout of
+// include/orcg_reader.h: (field, bytes) pairs; col_field reads / rebinds one.
+enum ColField { kFNn, kFData, kFLength, kFOffsets, kFBlob, kFSecondary, kFTags, kFIndex, kFDictOffsets };
+static void col_buffers(const ColOut& o, const TypeInfo& t, std::vector<std::pair<int, uint64_t>>& b) {
+  const uint64_t n = o.n;
+  auto add = [&](int f, const void* p, uint64_t bytes) {
+    if (p && bytes) b.push_back({f, bytes});
+  };
+  if (o.has_nulls) add(kFNn, o.nn, n);
+  const uint32_t k = o.kind;
+  if (k == ORCG_TYPE_DECIMAL) {
+    add(kFData, o.data, (t.precision > 18 || t.precision == 0 ? 16 : 8) * n);
+  } else if (k == ORCG_TYPE_LIST || k == ORCG_TYPE_MAP) {
+    add(kFOffsets, o.offsets, 8 * (n + 1));
+  } else if (k == ORCG_TYPE_UNION) {
+    add(kFTags, o.tags, n);
+    add(kFOffsets, o.offsets, 8 * n);
+  } else if (k != ORCG_TYPE_STRUCT) {
+    add(kFData, o.data, 8 * n);
+  }
+  add(kFLength, o.length, 8 * n);
+  add(kFSecondary, o.secondary, 8 * n);
+  add(kFIndex, o.index, 8 * n);
+  add(kFDictOffsets, o.dict_offsets, 8 * (o.dict_size + 1));
+  add(kFBlob, o.blob, o.blob_len);
+}
+static const void* col_get(const ColOut& o, int f) {
+  switch (f) {
+    case kFNn: return o.nn;
+    case kFData: return o.data;
+    case kFLength: return o.length;
+    case kFOffsets: return o.offsets;
+    case kFBlob: return o.blob;
+    case kFSecondary: return o.secondary;
+    case kFTags: return o.tags;
+    case kFIndex: return o.index;
+    default: return o.dict_offsets;
+  }
+}
+static void col_set(ColOut& o, int f, const void* p) {
+  switch (f) {
+    case kFNn: o.nn = (const uint8_t*)p; break;
+    case kFData: o.data = p; break;
+    case kFLength: o.length = (const int64_t*)p; break;
+    case kFOffsets: o.offsets = (const int64_t*)p; break;
+    case kFBlob: o.blob = (const uint8_t*)p; break;
+    case kFSecondary: o.secondary = (const int64_t*)p; break;
+    case kFTags: o.tags = (const uint8_t*)p; break;
+    case kFIndex: o.index = (const int64_t*)p; break;
+    default: o.dict_offsets = (const int64_t*)p; break;
+  }
+}
+
 struct orcg_row_reader {
   orcg_reader* r = nullptr;
+  // this row reader's RowReaderOptions
+  std::vector<uint8_t> selected;
+  bool lazy_dict = false;
   uint64_t nstripes = 0, first = 0, last = 0;  // stripes [first, last) are in range
   uint64_t current = 0, row_in_stripe = 0, rows_in_stripe = 0;
   uint64_t previous_row = 0;
   std::vector<uint64_t> first_row;  // firstRowOfStripe_
-  uint64_t loaded = ~0ull;          // stripe decoded in the reader's slot 0
   uint64_t batch_stripe = ~0ull, batch_row0 = 0, batch_rows = 0;
   std::vector<uint64_t> begin, count;  // per type id: element range of the current batch
   std::vector<uint8_t> in_batch;
+  const HostSlab* cur = nullptr;  // the slab of the current batch
+
+  // decode pipeline: host stages, one device slot, two host slabs (stripe
+  // s in slab s & 1); slab_state 0 empty, 1 queued / decoding, 2 ready
+  HostStage stage[2];
+  uint64_t prepared[2] = {~0ull, ~0ull};
+  std::unique_ptr<DevSlot> dev{new DevSlot()};
+  HostSlab slab[2];
+  int slab_state[2] = {0, 0};
+  uint64_t slab_want[2] = {~0ull, ~0ull};
+  std::thread worker;
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<uint64_t> jobs;
+  bool stop = false;
+
+  ~orcg_row_reader() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      stop = true;
+      jobs.clear();
+    }
+    cv.notify_all();
+    if (worker.joinable()) worker.join();
+  }
 
   void mark_end_of_file() {
     current = last;
@@ -1297,55 +1404,181 @@ struct orcg_row_reader {
     rows_in_stripe = 0;
     previous_row = last == 0 ? 0 : first_row[last - 1] + r->footer.stripes[last - 1].num_rows;
   }
-  int load(uint64_t s) {
-    if (loaded == s && r->nslots >= 1 && r->slots[0]->stripe == s) return ORCG_OK;
-    loaded = ~0ull;
-    const int rc = r->read_stripes(s, 1);
-    if (rc) return rc;
-    loaded = s;
-    return ORCG_OK;
-  }
-  int d2h(void* dst, const void* src, uint64_t bytes) {
-    int rc = hip_check(r->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, r->ctx->stream), "D2H");
-    if (!rc) rc = sync_ctx(r->ctx);
+
+  // --- worker side -------------------------------------------------------
+  struct OptsSwap {  // this row reader's options on the reader for one decode
+    // (copied, not swapped: the caller thread reads the row reader's own
+    // selection meanwhile)
+    orcg_reader* r;
+    std::vector<uint8_t> sel;
+    bool lazy;
+    OptsSwap(orcg_reader* r_, const orcg_row_reader* rr) : r(r_), sel(r_->selected), lazy(r_->lazy_dict) {
+      r->selected = rr->selected;
+      r->lazy_dict = rr->lazy_dict;
+    }
+    ~OptsSwap() {
+      r->selected.swap(sel);
+      r->lazy_dict = lazy;
+    }
+  };
+  // D2H of every decoded column of `dev` into the slab (one synchronisation)
+  int copy_out(HostSlab& sl) {
+    sl.out = dev->out;
+    // (column, field, bytes) of every decoded buffer
+    std::vector<std::pair<size_t, std::pair<int, uint64_t>>> bufs;
+    std::vector<std::pair<int, uint64_t>> cb;
+    for (size_t i = 0; i < sl.out.size(); ++i) {
+      if (!sl.out[i].decoded) continue;
+      cb.clear();
+      col_buffers(sl.out[i], r->footer.types[i], cb);
+      for (auto& x : cb) bufs.push_back({i, x});
+    }
+    uint64_t total = 0;
+    for (auto& bb : bufs) total += (bb.second.second + 255) & ~(uint64_t)255;
+    if (total > sl.cap) {
+      if (sl.h) (void)hipHostFree(sl.h);
+      sl.h = nullptr;
+      sl.cap = 0;
+      const uint64_t ncap = std::max<uint64_t>(total + (total >> 3), 1 << 20);
+      if (hipHostMalloc((void**)&sl.h, ncap, hipHostMallocDefault) != hipSuccess)
+        return r->fail(ORCG_OUT_OF_MEMORY, "pinned row batch allocation failed");
+      sl.cap = ncap;
+    }
+    uint64_t w = 0;
+    for (auto& bb : bufs) {
+      ColOut& o = sl.out[bb.first];
+      const int f = bb.second.first;
+      const uint64_t bytes = bb.second.second;
+      int rc = hip_check(r->ctx, hipMemcpyAsync(sl.h + w, col_get(o, f), bytes, hipMemcpyDeviceToHost, r->ctx->stream),
+                         "D2H row batch");
+      if (rc) return r->fail_ctx(rc);
+      col_set(o, f, sl.h + w);  // the slab's view points at host memory
+      w += (bytes + 255) & ~(uint64_t)255;
+    }
+    const int rc = sync_ctx(r->ctx);
     return rc ? r->fail_ctx(rc) : ORCG_OK;
   }
+  void run_job(uint64_t t) {
+    HostSlab& sl = slab[t & 1];
+    HostStage& hs = stage[t & 1];
+    int rc;
+    std::string err;
+    {
+      std::lock_guard<std::mutex> lk(r->mu);
+      OptsSwap sw(r, this);
+      (void)hipSetDevice(r->ctx->device);
+      rc = ORCG_OK;
+      if (prepared[t & 1] != t) {
+        prepared[t & 1] = t;
+        rc = r->prepare(t, hs);
+      } else {
+        rc = hs.rc;
+      }
+      if (rc) err = hs.err;
+      if (!rc) {
+        rc = r->upload_and_decode(hs, *dev);
+        if (!rc) rc = copy_out(sl);
+        if (rc) err = r->last_error;
+      }
+      prepared[t & 1] = ~0ull;  // the stage is reused by stripe t + 2
+    }
+    {
+      std::lock_guard<std::mutex> lk(m);
+      sl.stripe = t;
+      sl.rc = rc;
+      sl.err = err;
+      slab_state[t & 1] = 2;
+    }
+    cv.notify_all();
+    // host work ahead: decompress stripe t + 1 while the caller consumes
+    const uint64_t u = t + 1;
+    if (u < last && prepared[u & 1] != u) {
+      bool idle;
+      {
+        std::lock_guard<std::mutex> lk(m);
+        idle = jobs.empty() && !stop;
+      }
+      if (idle) {
+        std::lock_guard<std::mutex> lk(r->mu);
+        OptsSwap sw(r, this);
+        prepared[u & 1] = u;
+        (void)r->prepare(u, stage[u & 1]);  // a failure is kept in the stage
+      }
+    }
+  }
+  void loop() {
+    for (;;) {
+      uint64_t t;
+      {
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return stop || !jobs.empty(); });
+        if (stop) return;
+        t = jobs.front();
+        jobs.pop_front();
+      }
+      run_job(t);
+    }
+  }
+  // queue stripe t into slab t & 1 (caller holds m)
+  void post(std::unique_lock<std::mutex>& lk, uint64_t t) {
+    // a queued / running decode into the same slab finishes first
+    cv.wait(lk, [&] { return slab_state[t & 1] != 1; });
+    slab_state[t & 1] = 1;
+    slab_want[t & 1] = t;
+    jobs.push_back(t);
+    if (!worker.joinable()) worker = std::thread([this] { loop(); });
+    cv.notify_all();
+  }
+
+  // --- caller side -------------------------------------------------------
+  // make stripe s current (decoding it now if it is not already on its way),
+  // then start the decode of s + 1
+  int load(uint64_t s) {
+    std::unique_lock<std::mutex> lk(m);
+    HostSlab& sl = slab[s & 1];
+    const bool mine = (slab_state[s & 1] == 2 && sl.stripe == s) || (slab_state[s & 1] == 1 && slab_want[s & 1] == s);
+    if (!mine) post(lk, s);
+    cv.wait(lk, [&] { return slab_state[s & 1] == 2; });
+    if (sl.rc) {
+      const int rc = sl.rc;
+      r->last_error = sl.err;
+      slab_state[s & 1] = 0;  // a later seek decodes it again
+      cur = nullptr;
+      return rc;
+    }
+    cur = &sl;
+    const uint64_t u = s + 1;
+    if (u < last && !((slab_state[u & 1] == 2 && slab[u & 1].stripe == u) ||
+                      (slab_state[u & 1] == 1 && slab_want[u & 1] == u)))
+      post(lk, u);
+    return ORCG_OK;
+  }
   // element range [b, b + c) of column `id` and, recursively, its children
-  int ranges(uint32_t id, uint64_t b, uint64_t c) {
-    const ColOut& o = r->slots[0]->out[id];
-    if (!o.decoded) return ORCG_OK;
+  void ranges(uint32_t id, uint64_t b, uint64_t c) {
+    const ColOut& o = cur->out[id];
+    if (!o.decoded) return;
     begin[id] = b;
     count[id] = c;
     in_batch[id] = 1;
     const auto& t = r->footer.types[id];
-    int rc;
     if (t.kind == ORCG_TYPE_STRUCT) {
-      for (uint32_t st : t.subtypes)
-        if ((rc = ranges(st, b, c))) return rc;
+      for (uint32_t st : t.subtypes) ranges(st, b, c);
     } else if (t.kind == ORCG_TYPE_LIST || t.kind == ORCG_TYPE_MAP) {
-      int64_t ends[2] = {0, 0};
-      if ((rc = d2h(&ends[0], o.offsets + b, 8)) || (rc = d2h(&ends[1], o.offsets + b + c, 8))) return rc;
-      for (uint32_t st : t.subtypes)
-        if ((rc = ranges(st, (uint64_t)ends[0], (uint64_t)(ends[1] - ends[0])))) return rc;
+      const int64_t e0 = o.offsets[b], e1 = o.offsets[b + c];
+      for (uint32_t st : t.subtypes) ranges(st, (uint64_t)e0, (uint64_t)(e1 - e0));
     } else if (t.kind == ORCG_TYPE_UNION) {
       // child k's rows are the ranks of this batch's non-null tag-k rows
-      std::vector<uint8_t> tags(c), nn(c, 1);
-      std::vector<int64_t> offs(c);
-      if (c && ((rc = d2h(tags.data(), o.tags + b, c)) || (rc = d2h(offs.data(), o.offsets + b, 8 * c)) ||
-                (o.has_nulls && (rc = d2h(nn.data(), o.nn + b, c)))))
-        return rc;
       for (uint32_t k = 0; k < t.subtypes.size(); ++k) {
         uint64_t cb = ~0ull, cc = 0;
-        for (uint64_t i = 0; i < c; ++i)
-          if (nn[i] && tags[i] == k) {
-            if (cb == ~0ull) cb = (uint64_t)offs[i];
+        for (uint64_t i = b; i < b + c; ++i)
+          if ((!o.has_nulls || o.nn[i]) && o.tags[i] == k) {
+            if (cb == ~0ull) cb = (uint64_t)o.offsets[i];
             ++cc;
           }
         if (cb == ~0ull) cb = 0;  // no row of this batch carries tag k: an empty range
-        if ((rc = ranges(t.subtypes[k], cb, cc))) return rc;
+        ranges(t.subtypes[k], cb, cc);
       }
     }
-    return ORCG_OK;
   }
 };
 
@@ -1435,6 +1668,7 @@ const uint8_t* orcg_reader_metadata_value(const orcg_reader* r, uint32_t i, uint
 }
 int orcg_reader_set_lazy_dictionary(orcg_reader* r, int on) {
   if (!r) return ORCG_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(r->mu);
   r->lazy_dict = on != 0;
   return ORCG_OK;
 }
@@ -1484,31 +1718,39 @@ int orcg_reader_stripe(const orcg_reader* r, uint64_t s, orcg_stripe_info* out) 
   return ORCG_OK;
 }
 
-int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes) {
-  if (!r) return ORCG_INVALID_ARGUMENT;
-  const size_t nt = r->selected.size();
-  if (!include) {
-    for (auto& c : r->selected) c = 1;
-    return ORCG_OK;
-  }
+// RowReaderOptions::include by type id: the columns, their subtrees and
+// their ancestors (NULL = every column)
+static int compute_selection(orcg_reader* r, const uint8_t* include, uint32_t ntypes, std::vector<uint8_t>& sel) {
+  const size_t nt = r->footer.types.size();
+  sel.assign(nt, 1);
+  if (!include) return ORCG_OK;
   if (ntypes > nt) return r->fail(ORCG_INVALID_ARGUMENT, "include list longer than the type list");
   std::vector<uint32_t> parent(nt, 0);
   for (size_t i = 0; i < nt; ++i)
     for (uint32_t st : r->footer.types[i].subtypes) parent[st] = (uint32_t)i;
-  for (auto& c : r->selected) c = 0;
-  r->selected[0] = 1;
+  for (auto& c : sel) c = 0;
+  sel[0] = 1;
   for (uint32_t i = 0; i < ntypes; ++i) {
     if (!include[i]) continue;
-    // the column, its subtree and its ancestors
-    for (uint32_t a = i; a != 0; a = parent[a]) r->selected[a] = 1;
+    for (uint32_t a = i; a != 0; a = parent[a]) sel[a] = 1;
     std::vector<uint32_t> st{i};
     while (!st.empty()) {
       const uint32_t x = st.back();
       st.pop_back();
-      r->selected[x] = 1;
+      sel[x] = 1;
       for (uint32_t y : r->footer.types[x].subtypes) st.push_back(y);
     }
   }
+  return ORCG_OK;
+}
+
+int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  std::vector<uint8_t> sel;
+  const int rc = compute_selection(r, include, ntypes, sel);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(r->mu);
+  r->selected.swap(sel);
   return ORCG_OK;
 }
 
@@ -1518,11 +1760,13 @@ int orcg_reader_is_selected(const orcg_reader* r, uint32_t type_id) {
 
 int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe) {
   if (!r) return ORCG_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(r->mu);
   return r->read_stripes(stripe, 1);
 }
 
 int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count) {
   if (!r) return ORCG_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(r->mu);
   return r->read_stripes(first, count);
 }
 
@@ -1569,13 +1813,11 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
   if (!r->ctx) return r->fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
   const uint64_t off = o ? o->offset : 0;
   const uint64_t len = o ? o->length : ~0ull;
-  if (o) {
-    int rc = orcg_reader_select(r, o->include, o->include ? o->include_len : 0);
-    if (rc) return rc;
-    r->lazy_dict = o->lazy_dictionary != 0;
-  }
   std::unique_ptr<orcg_row_reader> rr(new orcg_row_reader());
   rr->r = r;
+  int rc = compute_selection(r, o ? o->include : nullptr, o && o->include ? o->include_len : 0, rr->selected);
+  if (rc) return rc;
+  rr->lazy_dict = o && o->lazy_dictionary != 0;
   const uint64_t ns = r->footer.stripes.size();
   rr->nstripes = ns;
   rr->current = ns;
@@ -1606,6 +1848,10 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
 
 void orcg_row_reader_destroy(orcg_row_reader* rr) { delete rr; }
 
+int orcg_row_reader_is_selected(const orcg_row_reader* rr, uint32_t type_id) {
+  return rr && type_id < rr->selected.size() && rr->selected[type_id] ? 1 : 0;
+}
+
 int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows) {
   if (!rr || !rows) return ORCG_INVALID_ARGUMENT;
   *rows = 0;
@@ -1616,8 +1862,8 @@ int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows)
     return ORCG_OK;
   }
   int rc;
-  if (rr->row_in_stripe == 0 || rr->loaded != rr->current) {
-    // startNextStripe
+  if (rr->row_in_stripe == 0 || !rr->cur || rr->cur->stripe != rr->current) {
+    // startNextStripe (its slab was decoded ahead while the last one was read)
     if ((rc = rr->load(rr->current))) return rc;
     rr->rows_in_stripe = rr->r->footer.stripes[rr->current].num_rows;
   }
@@ -1629,7 +1875,7 @@ int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows)
   rr->batch_stripe = rr->current;
   rr->batch_row0 = rr->row_in_stripe;
   rr->batch_rows = n;
-  if ((rc = rr->ranges(0, rr->row_in_stripe, n))) return rc;
+  rr->ranges(0, rr->row_in_stripe, n);
   rr->previous_row = rr->first_row[rr->current] + rr->row_in_stripe;
   rr->row_in_stripe += n;
   if (rr->row_in_stripe >= rr->rows_in_stripe) {
@@ -1641,6 +1887,8 @@ int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows)
 }
 
 uint64_t orcg_row_reader_row_number(const orcg_row_reader* rr) { return rr ? rr->previous_row : 0; }
+
+uint64_t orcg_row_reader_stripe(const orcg_row_reader* rr) { return rr ? rr->batch_stripe : ~0ull; }
 
 int orcg_row_reader_seek_to_row(orcg_row_reader* rr, uint64_t row) {
   if (!rr) return ORCG_INVALID_ARGUMENT;
@@ -1675,9 +1923,24 @@ int orcg_row_reader_column(const orcg_row_reader* rr, uint32_t id, orcg_column_v
   view->type_id = id;
   view->kind = rr->r->footer.types[id].kind;
   *begin = *count = 0;
-  if (!rr->in_batch[id]) return ORCG_OK;  // no batch, or the column is not decoded
-  const int rc = orcg_reader_stripe_column(rr->r, 0, id, view);
-  if (rc) return rc;
+  if (!rr->in_batch[id] || !rr->cur) return ORCG_OK;  // no batch, or the column is not decoded
+  const ColOut& c = rr->cur->out[id];
+  view->encoding = c.encoding;
+  view->decoded = c.decoded ? 1u : 0u;
+  if (!c.decoded) return ORCG_OK;
+  view->num_elements = c.n;
+  view->has_nulls = c.has_nulls ? 1 : 0;
+  view->not_null = c.nn;
+  view->data = c.data;
+  view->length = c.length;
+  view->offsets = c.offsets;
+  view->blob = c.blob;
+  view->blob_len = c.blob_len;
+  view->secondary = c.secondary;
+  view->tags = c.tags;
+  view->index = c.index;
+  view->dict_offsets = c.dict_offsets;
+  view->dict_size = c.dict_size;
   *begin = rr->begin[id];
   *count = rr->count[id];
   return ORCG_OK;

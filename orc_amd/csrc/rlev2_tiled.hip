@@ -89,7 +89,8 @@ constexpr int kOptFast = 8;     // predicate-free paths for full (512-value) run
 constexpr int kOptRegFill = 16; // fill windows through registers (16 B buffer loads, then LDS writes), not LDS-DMA
 constexpr int kOptT4 = 32;
 constexpr int kOptD3 = 64;      // dense discovery: predicated chain marks, wave-reduced control atomics, inline probe
-constexpr int kOptDirect = 128; // dense expansion: lanes store their short runs' values straight to the output (no stage)      // walk reads DELTA varint ends from per-dword terminator nibbles computed at slice load
+constexpr int kOptDirect = 128; // dense expansion: lanes store their short runs' values straight to the output (no stage)
+constexpr int kOptPair = 256;   // full DIRECT runs: two values per lane, one 16-byte store (16-byte aligned int64 output)
 
 // Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
 // counts the values of the runs it expands; each pass checks the count
@@ -110,6 +111,17 @@ template <int kOpt, typename T>
 __device__ __forceinline__ void store1(T* p, uint64_t v) {
   if constexpr ((kOpt & kOptNTStore) != 0) __builtin_nontemporal_store((T)(int64_t)v, p);
   else *p = (T)(int64_t)v;
+}
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+// two consecutive int64 values, one 16-byte store (p 16-byte aligned)
+template <int kOpt>
+__device__ __forceinline__ void store2(int64_t* p, uint64_t a, uint64_t b) {
+  u64x2 v;
+  v.x = a;
+  v.y = b;
+  if constexpr ((kOpt & kOptNTStore) != 0) __builtin_nontemporal_store(v, (u64x2*)p);
+  else *(u64x2*)p = v;
 }
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* w, uint32_t o) {
@@ -224,6 +236,44 @@ __device__ __forceinline__ void expand_run(const uint32_t* win, uint32_t nwords,
     if ((kOpt & kOptFast) && L == 512 && v0 >= value_begin && v0 + 512 <= value_end) {
       // Full run entirely inside the output range: no per-value predicates.
       T* out = dst + (v0 - value_begin);
+      if constexpr ((kOpt & kOptPair) != 0 && sizeof(T) == 8) {
+        if ((((uintptr_t)out) & 15u) == 0) {
+          // lane pairs of values: a wave stores 1 KB per instruction
+          if (W == 64) {
+            const uint32_t r4 = d & 3u;
+#pragma unroll
+            for (int it = 0; it < kMaxRunUnroll / 2; ++it) {
+              const uint32_t j = 2u * (uint32_t)(it * kWave + lane);
+              const uint32_t i = (d + 8u * j) >> 2;
+              const uint32_t w0 = win[i], w1 = win[i + 1], w2 = win[i + 2], w3 = win[i + 3], w4 = win[i + 4];
+              uint64_t a = ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, r4)) << 32) |
+                           __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, r4));
+              uint64_t b = ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w3, w2, r4)) << 32) |
+                           __builtin_bswap32(__builtin_amdgcn_alignbyte(w4, w3, r4));
+              if (is_signed) {
+                a = unzigzag(a);
+                b = unzigzag(b);
+              }
+              store2<kOpt>((int64_t*)out + j, a, b);
+            }
+          } else {
+#pragma unroll
+            for (int it = 0; it < kMaxRunUnroll / 2; ++it) {
+              const uint32_t j = 2u * (uint32_t)(it * kWave + lane);
+              const uint32_t bit = j * W, bit2 = bit + W;
+              const uint32_t br = d + (bit >> 3), br2 = d + (bit2 >> 3);
+              uint64_t a = field(lds12(win, br), br, bit & 7u, W);
+              uint64_t b = field(lds12(win, br2), br2, bit2 & 7u, W);
+              if (is_signed) {
+                a = unzigzag(a);
+                b = unzigzag(b);
+              }
+              store2<kOpt>((int64_t*)out + j, a, b);
+            }
+          }
+          return;
+        }
+      }
       if (W == 64) {
         // 8 bytes per value at d + 8j: one uniform byte alignment per run
         const uint32_t r4 = d & 3u;
@@ -1948,6 +1998,9 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     case 22: ORCG_KT(kSer, 12, false, 5, 2); break;                                    // dense v2, 12.5 KB
     case 23: ORCG_KT(kSer, 20, false, 4, 2); break;                                    // dense v2, 20.5 KB
     case 24: ORCG_KT(kWide, 32, false, 1, 2); break;                                   // dense v2, 32.5 KB
+    case 25: ORCG_KT(kWide | kOptPair, 33, false, 1, false); break;                    // 20 + 16-byte pair stores
+    case 26: ORCG_DEFERRING(kWide | kOptD3 | kOptPair, 33, 1, kSer | kOptD3 | kOptPair); break;  // 2 + pair stores
+    case 27: ORCG_KT(kSer | kOptPair, 21, false, 6, false); break;                     // 16 + pair stores
 #endif
     default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "unknown RLEv2 kernel variant");
   }
@@ -1998,12 +2051,16 @@ static int stage_jobs(Ctx* ctx, const RleJob* jobs, uint32_t n, const RleJob** o
   return hip_check(ctx, hipMemcpyAsync(d, h, n * sizeof(RleJob), hipMemcpyHostToDevice, ctx->stream), "H2D jobs");
 }
 
+bool rlev2_multi_capable(int variant) { return variant == 0 || (variant >= 2 && variant <= 7); }
+
 int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
   const int pinned = ctx->rlev2_variant;
-  if (pinned == ORCG_RLEV2_WAVE_WALK || (pinned != 0 && (pinned < 2 || pinned > 5))) {
-    // not a multi-stream instance: one launch per stream
+  if (!rlev2_multi_capable(pinned)) {
+    // not a multi-stream instance: one launch per stream (the reader queues
+    // only segment-table jobs for these variants, rlev2_multi_capable)
     for (uint32_t j = 0; j < njobs; ++j) {
       const RleJob& J = jobs[j];
+      if (!J.segtab) return set_error(ctx, ORCG_INVALID_ARGUMENT, "row-index job needs a multi-stream instance");
       int rc = launch_rlev2(ctx, J.src, J.src_len, (int)J.is_signed, J.segtab, J.nsegs, false, 0, 0, J.nvalues,
                             J.dst, 8);
       if (rc) return rc;
@@ -2011,7 +2068,7 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
     return ORCG_OK;
   }
   // one launch per instance: group the streams by the instance they get
-  std::vector<RleJob> group[6];
+  std::vector<RleJob> group[8];
   for (uint32_t j = 0; j < njobs; ++j) {
     const RleJob& J = jobs[j];
     if (J.nsegs == 0 || J.nvalues == 0) continue;
@@ -2019,12 +2076,12 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
   }
   static const bool dbg = getenv("ORCG_DEBUG_JOBS") != nullptr;
   if (dbg)
-    for (int v = 2; v <= 5; ++v)
+    for (int v = 2; v <= 7; ++v)
       for (const RleJob& J : group[v])
         fprintf(stderr, "rle job: instance %d bytes %llu values %llu segments %llu (%.3f B/value)\n", v,
                 (unsigned long long)J.src_len, (unsigned long long)J.nvalues, (unsigned long long)J.nsegs,
                 (double)J.src_len / (double)J.nvalues);
-  for (int v = 2; v <= 5; ++v) {
+  for (int v = 2; v <= 7; ++v) {
     std::vector<RleJob>& g = group[v];
     if (g.empty()) continue;
     // workgroups start in index order: the streams with the most stream

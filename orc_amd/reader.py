@@ -73,8 +73,9 @@ class ColumnBatch:
     """Host copy of one column's device batch."""
 
     def __init__(self, kind, n, not_null, data, length, offsets, blob, encoding, secondary=None, tags=None,
-                 index=None, dict_offsets=None):
+                 index=None, dict_offsets=None, scale=None):
         self.kind = kind
+        self.scale = scale          # DECIMAL: the scale the values were decoded at
         self.secondary = secondary  # np.int64[n] TIMESTAMP nanoseconds
         self.num_elements = n
         self.not_null = not_null  # np.uint8[n] or None
@@ -123,7 +124,7 @@ class Batch:
                 u = (hi << 64) | lo
             else:
                 u = int(c.data[i])
-            return decimal.Decimal(u).scaleb(-(t.scale if t.precision else self.reader.hive11_scale))
+            return decimal.Decimal(u).scaleb(-(c.scale if c.scale is not None else t.scale))
         if k in (TIMESTAMP, TIMESTAMP_INSTANT):
             # TimestampVectorBatch seconds + nanoseconds, as numpy datetime64[ns]
             return np.datetime64(int(c.data[i]) * 1_000_000_000 + int(c.secondary[i]), "ns")
@@ -268,11 +269,16 @@ class Reader:
         inc[list(type_ids)] = 1
         check(self._L.orcg_reader_select(self._h, inc.ctypes.data_as(ctypes.c_void_p), inc.size), self._err)
 
-    def _host(self, ptr, nbytes, dtype):
+    def _host(self, ptr, nbytes, dtype, from_host=False):
+        """Copy `nbytes` at `ptr` (device memory, or with from_host a row
+        reader's pinned host slab) into a new array."""
         out = np.empty(nbytes // np.dtype(dtype).itemsize, dtype=dtype)
         if nbytes:
-            check(self._L.orcg_reader_copy_to_host(self._h, out.ctypes.data_as(ctypes.c_void_p), ptr, nbytes),
-                  self._err)
+            if from_host:
+                ctypes.memmove(out.ctypes.data, ptr, nbytes)
+            else:
+                check(self._L.orcg_reader_copy_to_host(self._h, out.ctypes.data_as(ctypes.c_void_p), ptr, nbytes),
+                      self._err)
         return out
 
     def read_stripe_device(self, i):
@@ -301,18 +307,20 @@ class Reader:
         check(self._L.orcg_reader_stripe_column(self._h, k, tid, ctypes.byref(v)), self._err)
         return v
 
-    def _column(self, v, t, begin=0, count=None):
-        """Host copy of elements [begin, begin + count) of a device column
-        view (the whole column by default): offsets rebased to 0 (the
-        reference's batch layout), string starts relative to the copied blob
-        (the dictionary, or the span of direct strings the range covers)."""
+    def _column(self, v, t, begin=0, count=None, from_host=False, dict_cache=None):
+        """Host copy of elements [begin, begin + count) of a column view (the
+        whole column by default; device pointers, or with from_host a row
+        reader's host slab): offsets rebased to 0 (the reference's batch
+        layout), string starts relative to the copied blob (the dictionary,
+        or the span of direct strings the range covers). dict_cache (a dict)
+        keeps a dictionary's host copy for the next batches of the stripe."""
         n = v.num_elements if count is None else count
         k = t.kind
 
         def host(ptr, itemsize, dtype, cnt, first=begin):
             if not ptr or cnt <= 0:
                 return np.zeros(max(cnt, 0), dtype=dtype)
-            return self._host(ptr + first * itemsize, cnt * itemsize, dtype)
+            return self._host(ptr + first * itemsize, cnt * itemsize, dtype, from_host)
 
         nn = host(v.not_null, 1, np.uint8, n) if v.has_nulls else None
         data = length = offsets = tags = index = dict_offsets = secondary = None
@@ -322,14 +330,20 @@ class Reader:
         elif k in (BOOLEAN, BYTE, SHORT, INT, LONG, DATE):
             data = host(v.data, 8, np.int64, n)
         elif k in STRING_KINDS:
+            key = (t.id, v.dict_offsets, v.blob, v.dict_size, v.blob_len)
+            cached = dict_cache.get(key) if dict_cache is not None and v.index else None
             if v.index:
                 index = host(v.index, 8, np.int64, n)
-                dict_offsets = self._host(v.dict_offsets, 8 * (v.dict_size + 1), np.int64)
+                dict_offsets = cached[0] if cached else \
+                    self._host(v.dict_offsets, 8 * (v.dict_size + 1), np.int64, from_host)
             if v.data:
                 data = host(v.data, 8, np.int64, n)
                 length = host(v.length, 8, np.int64, n)
             if v.index and v.dict_offsets:
-                blob = self._host(v.blob, v.blob_len, np.uint8).tobytes()  # the dictionary
+                # the dictionary
+                blob = cached[1] if cached else self._host(v.blob, v.blob_len, np.uint8, from_host).tobytes()
+                if dict_cache is not None and not cached:
+                    dict_cache[key] = (dict_offsets, blob)
             elif data is not None and n:
                 live = length > 0
                 lo = int(data[live].min()) if live.any() else 0
@@ -345,11 +359,14 @@ class Reader:
         if k == DECIMAL:
             w = 16 if t.precision > 18 or t.precision == 0 else 8
             data = host(v.data, w, np.int64, n).reshape(-1) if w == 8 else \
-                self._host(v.data + begin * 16, 16 * n, np.int64) if n else np.zeros(0, np.int64)
+                self._host(v.data + begin * 16, 16 * n, np.int64, from_host) if n else np.zeros(0, np.int64)
         elif k in (TIMESTAMP, TIMESTAMP_INSTANT):
             data = host(v.data, 8, np.int64, n)
             secondary = host(v.secondary, 8, np.int64, n)
-        return ColumnBatch(k, n, nn, data, length, offsets, blob, v.encoding, secondary, tags, index, dict_offsets)
+        # Hive 0.11 decimals are decoded at the forced scale in effect now
+        scale = (t.scale if t.precision else self.hive11_scale) if k == DECIMAL else None
+        return ColumnBatch(k, n, nn, data, length, offsets, blob, v.encoding, secondary, tags, index, dict_offsets,
+                           scale)
 
     def read_stripe(self, i):
         """Decode stripe i on the GPU and copy the selected columns to host."""
@@ -397,11 +414,12 @@ class Reader:
         """RowReaderOptions::setEnableLazyDecoding for stripe reads."""
         check(self._L.orcg_reader_set_lazy_dictionary(self._h, int(bool(on))), self._err)
 
-    def create_row_reader(self, include=None, offset=0, length=None, lazy_dictionary=False):
+    def create_row_reader(self, include=None, offset=0, length=None, lazy_dictionary=False, tight_numeric=False):
         """Reader::createRowReader(RowReaderOptions): `include` type ids (or
         top-level field names), range(offset, length) in file bytes,
-        setEnableLazyDecoding."""
-        return RowReader(self, include=include, offset=offset, length=length, lazy_dictionary=lazy_dictionary)
+        setEnableLazyDecoding, setUseTightNumericVector."""
+        return RowReader(self, include=include, offset=offset, length=length, lazy_dictionary=lazy_dictionary,
+                         tight_numeric=tight_numeric)
 
     def last_timings(self):
         t = (ctypes.c_double * 5)()
@@ -430,6 +448,11 @@ class Reader:
         return rows
 
 
+# setUseTightNumericVector batch element types (c++/src/ColumnReader.cc:1703-1790,
+# c++/src/TypeImpl.cc createRowBatch)
+_TIGHT = {BOOLEAN: np.int8, BYTE: np.int8, SHORT: np.int16, INT: np.int32, FLOAT: np.float32}
+
+
 class RowBatch(Batch):
     """A batch of at most `capacity` rows (RowReader::createRowBatch)."""
 
@@ -451,7 +474,7 @@ class RowReader:
     seek_to_row follow RowReaderImpl (:424-499); range(offset, length)
     selects the stripes whose offset falls in the byte range (:337-345)."""
 
-    def __init__(self, reader, include=None, offset=0, length=None, lazy_dictionary=False):
+    def __init__(self, reader, include=None, offset=0, length=None, lazy_dictionary=False, tight_numeric=False):
         if reader._ctx is None:
             raise _lib.InvalidArgument("reader was opened without a device context")
         self.reader = reader
@@ -471,6 +494,13 @@ class RowReader:
         h = ctypes.c_void_p()
         check(self._L.orcg_row_reader_create(reader._h, ctypes.byref(opts), ctypes.byref(h)), reader._err)
         self._h = h
+        self.tight_numeric = tight_numeric
+        self._dicts = {}  # the current stripe's dictionaries (host copies)
+        self._dict_stripe = None
+
+    def is_selected(self, tid):
+        """RowReader::getSelectedColumns()[tid]."""
+        return bool(self._L.orcg_row_reader_is_selected(self._h, tid))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -491,6 +521,9 @@ class RowReader:
         batch.columns = {}
         if rows.value == 0:
             return False
+        stripe = self._L.orcg_row_reader_stripe(self._h)
+        if stripe != self._dict_stripe:
+            self._dicts, self._dict_stripe = {}, stripe
         begins = {}
         for t in self.reader.types:
             v = _lib.ColumnView()
@@ -498,7 +531,12 @@ class RowReader:
             check(self._L.orcg_row_reader_column(self._h, t.id, ctypes.byref(v), ctypes.byref(b), ctypes.byref(c)),
                   self.reader._err)
             if v.decoded:
-                batch.columns[t.id] = self.reader._column(v, t, b.value, c.value)
+                col = self.reader._column(v, t, b.value, c.value, from_host=True, dict_cache=self._dicts)
+                if self.tight_numeric and t.kind in _TIGHT:
+                    # RowReaderOptions::setUseTightNumericVector: Byte / Short /
+                    # Int / FloatVectorBatch (ColumnReader.cc:1703-1790)
+                    col.data = col.data.astype(_TIGHT[t.kind])
+                batch.columns[t.id] = col
                 begins[t.id] = b.value
         # union offsets index the stripe's child rows: make them batch-relative
         for tid, col in batch.columns.items():

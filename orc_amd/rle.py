@@ -369,6 +369,42 @@ class ByteRleDecoder:
             pass
 
 
+def java_tree_present_next(present, batch, parent_is_null=None, is_repeating=False):
+    """TreeReader.nextVector (TreeReaderFactory.java:405-441) through the C
+    ABI: `present` a boolean ByteRleDecoder (BitFieldReader) or None; returns
+    (isNull bytes, noNulls, isRepeating)."""
+    L = _lib.load()
+    isn = np.zeros(batch, dtype=np.uint8)
+    par = None if parent_is_null is None else np.ascontiguousarray(parent_is_null, dtype=np.uint8)
+    nn, rep = ctypes.c_int(0), ctypes.c_int(1 if is_repeating else 0)
+    check(L.orcg_java_tree_present_next(present._h if present is not None else None, _ptr(par), batch, _ptr(isn),
+                                        ctypes.byref(nn), ctypes.byref(rep)), L.orcg_java_last_error)
+    return isn, bool(nn.value), bool(rep.value)
+
+
+def java_dictionary_next(data, dict_offsets, buffer_len, is_null, no_nulls, is_repeating, scratch,
+                         has_buffer=True, start=None, length=None):
+    """StringDictionaryTreeReader.readDictionaryByteArray
+    (TreeReaderFactory.java:2396-2478): `data` the DATA RleDecoderV2
+    (unsigned), dict_offsets the int[] dictionaryOffsets (None = null),
+    is_null / no_nulls / is_repeating from java_tree_present_next (is_null is
+    updated in place), scratch the persistent scratchlcv.vector (int64).
+    Returns (start, length, noNulls, isRepeating): the setRef arguments."""
+    L = _lib.load()
+    batch = is_null.size
+    offs = None if dict_offsets is None else np.ascontiguousarray(dict_offsets, dtype=np.int32)
+    if start is None:
+        start = np.zeros(batch, dtype=np.int32)
+    if length is None:
+        length = np.zeros(batch, dtype=np.int32)
+    nn, rep = ctypes.c_int(1 if no_nulls else 0), ctypes.c_int(1 if is_repeating else 0)
+    check(L.orcg_java_dictionary_next(data._h if data is not None else None, _ptr(offs),
+                                      0 if offs is None else offs.size, 1 if has_buffer else 0, int(buffer_len),
+                                      _ptr(is_null), ctypes.byref(nn), ctypes.byref(rep), batch, _ptr(scratch),
+                                      _ptr(start), _ptr(length)), L.orcg_java_last_error)
+    return start, length, bool(nn.value), bool(rep.value)
+
+
 def create_byte_rle_decoder(data, ctx=None):
     return ByteRleDecoder(data, boolean=False, ctx=ctx)
 

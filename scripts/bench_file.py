@@ -61,6 +61,77 @@ def view_bytes(v, kind, precision):
     return b
 
 
+def concat_leg(dist, r, path, first, last, rank):
+    """The N > 1 final concat, timed apart from the decode: every rank copies
+    its stripes' rows of the first integer column out of HBM into its own
+    slice of one shared host batch (orc_amd.shard.write_rows_to_shared_host,
+    no data collective); rank 0 checks the assembled column against
+    pyarrow."""
+    import torch
+
+    from orc_amd.shard import write_rows_to_shared_host
+
+    root = r.types[0]
+    fields = [(n, t) for n, t in zip(root.field_names, root.subtypes) if r.types[t].kind in (2, 3, 4)]
+    if not fields:
+        return None
+    name, tid = fields[0]
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else os.environ.get("TMPDIR", "/tmp")
+    fpath = os.path.join(shm, "orcg_bench_file_concat_%s" % os.environ.get("MASTER_PORT", "0"))
+    dist.barrier()
+    t = time.perf_counter()
+    parts = []
+    for k in range(last - first):
+        v = r.stripe_column_view(k, tid)
+        parts.append(r._host(v.data, 8 * v.num_elements, np.int64))
+    local = torch.from_numpy(np.concatenate(parts) if parts else np.zeros(0, np.int64))
+    host = write_rows_to_shared_host(dist, local, fpath, create=(rank == 0))
+    el = time.perf_counter() - t
+    tt = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    ok = None
+    if rank == 0:
+        import pyarrow.orc as po
+        col = po.ORCFile(path).read(columns=[name]).column(0)
+        want = np.array([0 if x is None else x for x in col.to_pylist()], dtype=np.int64)
+        ok = bool(np.array_equal(host.numpy(), want))
+        if not ok:
+            raise SystemExit("concatenated %s differs from pyarrow" % name)
+    dist.barrier()
+    if rank == 0 and os.path.exists(fpath):
+        os.unlink(fpath)
+    n = int(host.numel())
+    return {"column": name, "rows": n, "ms": round(float(tt.item()) * 1e3, 3),
+            "GBps": round(8 * n / float(tt.item()) / 1e9, 2), "mode": "D2H into a shared host batch",
+            "checked_against_pyarrow": ok}
+
+
+def row_reader_leg(path, nrows, stripes_wall):
+    """The reference caller's path: orc::RowReader::next(batch) at capacity
+    1024 through the C++ adapter (orc_amd/csrc/GpuRowReader.hh), every batch
+    filled into host ColumnVectorBatches; a compiled program
+    (tests/cxx/reader_test.cpp --bench), timed from the first next() to the
+    last."""
+    import subprocess
+
+    src = os.path.join(ROOT, "tests", "cxx", "reader_test.cpp")
+    exe = os.path.join(ROOT, "tests", "cxx", "build", "reader_test")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", src, "-o",
+                               exe, "-L" + os.path.join(ROOT, "orc_amd"), "-lorcgpu",
+                               "-Wl,-rpath," + os.path.join(ROOT, "orc_amd"), "-Wl,-rpath,/opt/rocm/lib"])
+    out = {}
+    for cap in (1024,):
+        r = subprocess.run([exe, path, "--bench", "--batch", str(cap)], capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise SystemExit("row reader bench failed: %s" % r.stderr[-500:])
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        d["vs_read_stripes_wall"] = round(d["seconds"] / max(stripes_wall, 1e-9), 2)
+        out["batch_%d" % cap] = d
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
@@ -71,6 +142,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--host-copy", action="store_true", help="also time decode + D2H into host batches")
     ap.add_argument("--no-batch", action="store_true", help="one RLEv2 launch per stream (no multi-stream launches)")
+    ap.add_argument("--row-reader", action="store_true",
+                    help="also time the C++ RowReader scan loop (tests/cxx/reader_test --bench, batch 1024)")
+    ap.add_argument("--cpu-threads", default="1,16", help="pyarrow ORC reader thread counts for the CPU legs")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; gloo lets "
+                                                      "ranks share one GPU)")
     args = ap.parse_args()
     maker, default_rows, desc = WORKLOADS[args.workload]
     rows = args.rows or default_rows
@@ -87,18 +163,21 @@ def main():
 
     import torch
 
-    torch.cuda.set_device(local_rank)
+    torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(args.backend)
         dist.barrier()  # the file exists
 
     import orc_amd
     from orc_amd.shard import reader_ranges
 
-    ctx = orc_amd.Context(local_rank)
+    ctx = orc_amd.Context(local_rank % max(torch.cuda.device_count(), 1))
     r = orc_amd.Reader(path, ctx)
     if args.no_batch:
         r.set_stream_batching(False)
@@ -136,19 +215,26 @@ def main():
             if v.decoded:
                 dec_bytes += view_bytes(v, t.kind, t.precision)
 
+    concat = None
+    if dist:
+        concat = concat_leg(dist, r, path, first, last, rank)
+
     check = None
-    if rank == 0 and r.num_stripes:
-        # correctness spot check: stripe 0 against pyarrow (the reference C++ reader)
+    if last > first:
+        # correctness spot check on every rank: its first and last stripe
+        # against pyarrow (the reference C++ reader)
         import pyarrow.orc as po
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from file_parity import first_difference
 
-        got = r.read_stripe(0).to_pylist()
-        want = po.ORCFile(path).read_stripe(0).to_pylist()
-        diff = first_difference(want, got)
-        if diff:
-            raise SystemExit("%s decode mismatch against pyarrow: %s" % (args.workload, diff))
-        check = "stripe 0 (%d rows) equal to pyarrow" % len(got)
+        f = po.ORCFile(path)
+        for s_ in sorted({first, last - 1}):
+            got = r.read_stripe(s_).to_pylist()
+            diff = first_difference(f.read_stripe(s_).to_pylist(), got)
+            if diff:
+                raise SystemExit("%s stripe %d decode mismatch against pyarrow on rank %d: %s"
+                                 % (args.workload, s_, rank, diff))
+        check = "stripes %s (%d rows) equal to pyarrow" % (sorted({first, last - 1}), len(got))
 
     host = None
     if args.host_copy and rank == 0:
@@ -157,17 +243,28 @@ def main():
             r.read_stripe(s)
         host = time.perf_counter() - t
 
+    rowreader = None
+    if args.row_reader and rank == 0:
+        rowreader = row_reader_leg(path, nrows, wall)
+
     cpu = None
     if not args.no_cpu_baseline and rank == 0:
+        # the reference's C++ reader as pyarrow bundles it (ORC C++ 2.2.2):
+        # a full read of the same file to Arrow, like tools/src/FileScan.cc's
+        # scan loop (c++ ColumnVectorBatch -> Arrow arrays), on 1 and N threads
         import pyarrow as pa
         import pyarrow.orc as po
-        pa.set_cpu_count(1)
-        t = time.perf_counter()
-        po.ORCFile(path).read()
-        tc = time.perf_counter() - t
-        cpu = {"value": round(nrows / tc / 1e6, 2), "unit": "Mrows/s", "cores": 1, "kind": "reference",
-               "sample": "pyarrow %s (ORC C++ reader) full read of the same file to Arrow, 1 thread, %.2f s"
-                         % (pa.__version__, tc)}
+        legs = []
+        for th in [int(x) for x in args.cpu_threads.split(",") if x]:
+            pa.set_cpu_count(th)
+            t = time.perf_counter()
+            po.ORCFile(path).read()
+            tc = time.perf_counter() - t
+            legs.append({"value": round(nrows / tc / 1e6, 2), "unit": "Mrows/s", "cores": th,
+                         "kind": "pyarrow ORC C++ %s" % pa.__version__,
+                         "sample": "full read of the same file to Arrow (pyarrow.orc.ORCFile.read), "
+                                   "pa.set_cpu_count(%d), %.2f s" % (th, tc)})
+        cpu = dict(legs[0], all_legs=legs) if legs else None
 
     if rank == 0:
         line = {
@@ -190,6 +287,8 @@ def main():
             "device_vs_roofline": round(ph[4] / max((stats["stage_bytes"] + dec_bytes) / 6e12, 1e-12), 1),
             "rle_streams": stats,
             "host_batch_copy_s": None if host is None else round(host, 3),
+            "concat": concat,
+            "row_reader": rowreader,
             "check": check,
             "cpu_baseline": cpu,
             "make_file_s": round(t_make, 1),

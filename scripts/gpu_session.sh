@@ -65,6 +65,16 @@ for s in $STEPS; do
       for spec in ${SW_SPECS:-"random:64" "random:48" "random:13" "random:8" "random:1" "delta:12" "patched:12" "repeat:12" "repeat:40" "repeat:64" "shortdirect:16" "shortdirect:64" "shortmix:32"}; do
         run sw_${spec/:/_} 300 python scripts/ab_rlev2.py --data ${spec%%:*} --bits ${spec##*:} --variants $V --rounds 3 --refs copy,probe5 || true
       done ;;
+    tnew) run tnew 900 python -u -m pytest tests/test_gpu_java_tree.py tests/test_gpu_row_reader.py tests/test_cxx_adapter.py tests/test_gpu_reader.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    tfile) run tfile 900 python -u -m pytest ${TFILE_TESTS:-tests/test_gpu_reader.py} -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
+    bench5)
+      # the driver's settings (--steps 20 --warmup 5), variants interleaved
+      for v in ${B5_VARIANTS:-0 7 0 7}; do run bench5_v$v 300 python bench.py --steps 20 --warmup 5 --variant $v --no-cpu-baseline --copy-inclusive 0; cat $OUT/bench5_v$v.log >> $OUT/bench5_all.log; done ;;
+    ab64) run ab64 300 python scripts/ab_rlev2.py --data random --bits 64 --variants ${AB_VARIANTS:-0,2,7,20} --rounds 5 --refs copy,probe5 ;;
+    bf) for w in ${BF_WORKLOADS:-c5 c4 c3}; do run bf_$w 600 python scripts/bench_file.py --workload $w --row-reader ${BF_ARGS:-}; done ;;
+    proffile)
+      export TMPDIR=/tmp
+      for w in ${PF_WORKLOADS:-c5}; do run prof_$w 600 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_$w" -o run --output-format csv -- python3 scripts/bench_file.py --workload $w --iters 1 --no-cpu-baseline; done ;;
     benchwalk) run bench_walk 600 python bench.py --variant 1 --no-cpu-baseline ;;
     prof)
       export TMPDIR=/tmp

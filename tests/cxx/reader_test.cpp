@@ -6,7 +6,7 @@
 // (c++/src/ColumnPrinter.cc) so the Python test can compare every line with
 // examples/expected/*.jsn.gz.
 //
-//   reader_test <file.orc> [--batch N] [--seek r1,r2,...] [--range OFF LEN] [--lazy] [--include id,...]
+//   reader_test <file.orc> [--batch N] [--seek r1,r2,...] [--range OFF LEN] [--lazy] [--tight] [--bench] [--include id,...]
 //
 // --seek: for each row r, seekToRow(r) then one next(); prints "#seek r <getRowNumber>"
 //         before the batch's rows.
@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <ctime>
 #include <string>
 
@@ -102,12 +103,22 @@ static std::string value(const ColumnVectorBatch& b, uint64_t i, const std::vect
     if (b.kind == ORCG_TYPE_DATE) return date_str(l->data[i]);
     return std::to_string(l->data[i]);
   }
-  if (auto* d = dynamic_cast<const DoubleVectorBatch*>(&b)) {
-    if (std::isnan(d->data[i])) return "NaN";
-    if (std::isinf(d->data[i])) return d->data[i] > 0 ? "Infinity" : "-Infinity";
+  // setUseTightNumericVector batches print as their wide counterparts
+  if (auto* x = dynamic_cast<const IntVectorBatch*>(&b)) return std::to_string(x->data[i]);
+  if (auto* x = dynamic_cast<const ShortVectorBatch*>(&b)) return std::to_string(x->data[i]);
+  if (auto* x = dynamic_cast<const ByteVectorBatch*>(&b)) {
+    if (b.kind == ORCG_TYPE_BOOLEAN) return x->data[i] ? "true" : "false";
+    return std::to_string(x->data[i]);
+  }
+  const DoubleVectorBatch* dv = dynamic_cast<const DoubleVectorBatch*>(&b);
+  const FloatVectorBatch* fv = dynamic_cast<const FloatVectorBatch*>(&b);
+  if (dv || fv) {
+    const double x = dv ? dv->data[i] : (double)fv->data[i];
+    if (std::isnan(x)) return "NaN";
+    if (std::isinf(x)) return x > 0 ? "Infinity" : "-Infinity";
     // DoubleColumnPrinter (ColumnPrinter.cc:345-353): %.7g for FLOAT, %.14g for DOUBLE
     char buf[64];
-    snprintf(buf, sizeof buf, b.kind == ORCG_TYPE_FLOAT ? "%.7g" : "%.14g", d->data[i]);
+    snprintf(buf, sizeof buf, b.kind == ORCG_TYPE_FLOAT ? "%.7g" : "%.14g", x);
     return buf;
   }
   if (auto* s = dynamic_cast<const StringVectorBatch*>(&b)) {
@@ -154,9 +165,23 @@ static std::string value(const ColumnVectorBatch& b, uint64_t i, const std::vect
   return "null";
 }
 
+static const RowReader* g_rows = nullptr;  // the row reader's selection (RowReader::getSelectedColumns)
+
+// the children a batch holds: a struct's selected fields, every other child
+static std::vector<uint32_t> batch_subs(const Reader& r, uint32_t id) {
+  std::vector<uint32_t> out;
+  for (uint32_t s : r.getSubtypes(id))
+    if (r.getType(id).kind != ORCG_TYPE_STRUCT || g_rows->isSelected(s)) out.push_back(s);
+  return out;
+}
+
 // selected field names of every struct in the type tree, by type id
 static void names_of(const Reader& r, uint32_t id, std::vector<std::vector<std::string>>& out) {
-  if (r.getType(id).kind == ORCG_TYPE_STRUCT) out[id] = r.getSelectedFieldNames(id);
+  if (r.getType(id).kind == ORCG_TYPE_STRUCT) {
+    const auto subs = r.getSubtypes(id);
+    for (uint32_t i = 0; i < subs.size(); ++i)
+      if (g_rows->isSelected(subs[i])) out[id].push_back(r.getFieldName(id, i));
+  }
   for (uint32_t s : r.getSubtypes(id)) names_of(r, s, out);
 }
 
@@ -165,7 +190,7 @@ static std::vector<std::vector<std::string>> g_names;
 // value() with nested struct field names (walks the batch tree alongside the type tree)
 static std::string row(const Reader& r, uint32_t id, const ColumnVectorBatch& b, uint64_t i) {
   if (b.hasNulls && !b.notNull[i]) return "null";
-  const auto subs = r.getType(id).kind == ORCG_TYPE_STRUCT ? r.getSelectedSubtypes(id) : r.getSubtypes(id);
+  const auto subs = batch_subs(r, id);
   if (auto* sb = dynamic_cast<const StructVectorBatch*>(&b)) {
     std::string s = "{";
     for (size_t f = 0; f < sb->fields.size(); ++f) {
@@ -204,10 +229,12 @@ int main(int argc, char** argv) {
   uint64_t cap = 1024;
   std::vector<uint64_t> seeks;
   RowReaderOptions opts;
-  bool ranged = false;
+  bool ranged = false, bench = false;
   for (int a = 2; a < argc; ++a) {
     if (!strcmp(argv[a], "--batch") && a + 1 < argc) cap = strtoull(argv[++a], nullptr, 10);
     else if (!strcmp(argv[a], "--lazy")) opts.setEnableLazyDecoding(true);
+    else if (!strcmp(argv[a], "--tight")) opts.setUseTightNumericVector(true);
+    else if (!strcmp(argv[a], "--bench")) bench = true;
     else if (!strcmp(argv[a], "--include") && a + 1 < argc) {
       std::list<uint64_t> ids;
       char* p = argv[++a];
@@ -233,6 +260,7 @@ int main(int argc, char** argv) {
     Context ctx(0);
     Reader reader(ctx, argv[1]);
     auto rows = reader.createRowReader(opts);
+    g_rows = rows.get();
     g_names.assign(orcg_reader_num_types(reader.get()), {});
     names_of(reader, 0, g_names);
     auto batch = rows->createRowBatch(cap);
@@ -246,6 +274,20 @@ int main(int argc, char** argv) {
         for (uint64_t i = 0; more && i < batch->numElements; ++i) puts(row(reader, 0, *batch, i).c_str());
       }
       return 0;
+    }
+    if (bench) {
+      // the reference caller's scan loop (tools/src/FileScan.cc:22-44):
+      // next() until the end, every batch filled into host ColumnVectorBatches
+      const auto t0 = std::chrono::steady_clock::now();
+      uint64_t n = 0, batches = 0;
+      while (rows->next(*batch)) {
+        n += batch->numElements;
+        ++batches;
+      }
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      printf("{\"rows\": %llu, \"batches\": %llu, \"seconds\": %.6f, \"mrows_per_s\": %.3f}\n",
+             (unsigned long long)n, (unsigned long long)batches, s, n / s / 1e6);
+      return n == reader.getNumberOfRows() || ranged ? 0 : 1;
     }
     uint64_t total = 0;
     bool first = true;

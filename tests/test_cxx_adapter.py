@@ -185,3 +185,61 @@ def test_row_reader_adapter_range_and_lazy_decoding():
     assert len(rows) == firsts[5] - firsts[2]
     for k, g in enumerate(rows):
         assert printer_equal(want[int(firsts[2]) + k], g), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["TestOrcFile.test1.orc", "over1k_bloom.orc", "TestOrcFile.testSeek.orc"])
+def test_row_reader_adapter_tight_numeric_vectors(name):
+    """RowReaderOptions::setUseTightNumericVector (Reader.hh:375): BOOLEAN /
+    BYTE -> ByteVectorBatch, SHORT -> ShortVectorBatch, INT ->
+    IntVectorBatch, FLOAT -> FloatVectorBatch (ColumnReader.cc:1703-1790);
+    the rows print exactly as the reference's expected output."""
+    from file_parity import printer_equal
+
+    inc, want = _include(name)
+    got = _run_reader(name, "--batch", 777, "--include", inc, "--tight")
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert printer_equal(w, g), (name, i, w, g)
+
+
+@pytest.mark.gpu
+def test_two_row_readers_keep_their_own_options():
+    """Each RowReader keeps its RowReaderOptions (include, lazy decoding):
+    interleaving two of them, and a stripe read on the reader itself, changes
+    neither one's batches (options used to live on the reader)."""
+    import numpy as np
+
+    import orc_amd
+    from file_parity import path
+
+    r = orc_amd.Reader(path("TestOrcFile.testSeek.orc"), orc_amd.default_context(0))
+    root = r.types[0]
+    ids = dict(zip(root.field_names, root.subtypes))
+    a = r.create_row_reader(include=["int1", "string1"], lazy_dictionary=True)
+    b = r.create_row_reader(include=["long1"])
+    ba, bb = a.create_row_batch(3000), b.create_row_batch(2000)
+    rows_a, rows_b = [], []
+    more_a = more_b = True
+    k = 0
+    while more_a or more_b:
+        if more_a:
+            more_a = a.next(ba)
+            if more_a:
+                assert set(ba.columns) == {0, ids["int1"], ids["string1"]}
+                assert ba.columns[ids["string1"]].index is not None  # lazy: index + dictionary
+                rows_a.extend(ba.to_pylist(["int1", "string1"]))
+        if more_b:
+            more_b = b.next(bb)
+            if more_b:
+                assert set(bb.columns) == {0, ids["long1"]}
+                rows_b.extend(bb.to_pylist(["long1"]))
+        if k % 3 == 0:
+            r.read_stripe(k % r.num_stripes)  # the reader's own read in between
+        k += 1
+    assert len(rows_a) == len(rows_b) == r.num_rows
+    full = r.read()
+    assert rows_a == [{"int1": x["int1"], "string1": x["string1"]} for x in full]
+    assert rows_b == [{"long1": x["long1"]} for x in full]
+    assert a.is_selected(ids["int1"]) and not a.is_selected(ids["long1"])
+    assert np.all([b.is_selected(ids["long1"]), not b.is_selected(ids["int1"])])

@@ -165,3 +165,37 @@ def test_bench_two_ranks_on_one_gpu_with_gloo():
     d = lines[0]
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert "ms" in d["concat"]["host"], d["concat"]
+
+
+@pytest.mark.gpu
+def test_bench_file_two_ranks_sharded_c4():
+    """configs[3] sharded over two ranks (both on cuda:0, gloo): each rank
+    decodes its contiguous stripe range (RowReaderOptions::range,
+    c++/src/Reader.cc:337-345) and checks its first and last stripe against
+    pyarrow; the timed concat assembles l_orderkey in one shared host batch
+    that rank 0 checks against pyarrow; the JSON line reports the decode and
+    the concat separately."""
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    path = os.path.join("/tmp", "orcg_test_c4_2m_%d.orc" % os.getpid())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "scripts", "bench_file.py"),
+           "--workload", "c4", "--rows", "2000000", "--stripe-mb", "4", "--iters", "1", "--backend", "gloo",
+           "--no-cpu-baseline", "--path", path]
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env)
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(x) for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = lines[0]
+    assert d["config"]["n_gpus"] == 2 and d["config"]["stripes"] >= 4
+    assert d["concat"]["checked_against_pyarrow"] and d["concat"]["rows"] == 2_000_000
+    assert d["wall_s"] > 0 and d["concat"]["ms"] > 0
