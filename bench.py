@@ -124,6 +124,65 @@ def cpu_baseline(data, rows, budget_s):
     }
 
 
+def pyarrow_baseline(values, budget_s):
+    """The reference's own C++ reader as pyarrow bundles it (Apache ORC C++
+    2.2.2) on a C2-shaped file: the same full-range int64 values (a bounded
+    prefix) written uncompressed by pyarrow's ORC writer (RLEv2 DIRECT runs of
+    512 at W=64, 1 M-row stripes), read back stripe by stripe like
+    tools/src/FileScan.cc's scan loop, on 1 thread and on every usable core
+    (one stripe per task). Decoded GB/s = 8 B per value."""
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+
+    try:
+        import pyarrow as pa
+        import pyarrow.orc as po
+    except ImportError:
+        return None
+    n = min(values.size, 20_000_000)
+    fd, path = tempfile.mkstemp(suffix=".orc", dir=os.environ.get("TMPDIR", "/tmp"))
+    os.close(fd)
+    try:
+        po.write_table(pa.table({"v": pa.array(values[:n])}), path, compression="uncompressed",
+                       stripe_size=8 << 20, row_index_stride=10000)
+        nst = po.ORCFile(path).nstripes
+
+        def leg(threads, seconds):
+            # every thread reads its own stripes (k, k + threads, ...) with
+            # its own ORCFile, over and over, until the time is up
+            pa.set_cpu_count(threads)
+            t0 = time.perf_counter()
+            stop = t0 + seconds
+
+            def work(t):
+                f = po.ORCFile(path)
+                rows, k = 0, t % nst
+                while True:
+                    rows += f.read_stripe(k).num_rows
+                    k = (k + threads) % nst
+                    if time.perf_counter() >= stop:
+                        return rows
+
+            with ThreadPoolExecutor(threads) as ex:
+                done = sum(ex.map(work, range(threads)))
+            el = time.perf_counter() - t0
+            return done / el, done, el
+
+        cores = usable_cores()
+        v1, d1, e1 = leg(1, budget_s / 2)
+        vn, dn, en = leg(cores, budget_s / 2)
+        pa.set_cpu_count(cores)
+        return {"kind": "pyarrow ORC C++ (pyarrow %s)" % pa.__version__,
+                "sample": "first %d of the same values written uncompressed by pyarrow (%d stripes), read stripe "
+                          "by stripe" % (n, nst),
+                "one_core": {"value": round(v1 * 8 / 1e9, 3), "mvalues_per_s": round(v1 / 1e6, 1), "cores": 1,
+                             "rows_read": d1, "seconds": round(e1, 2)},
+                "all_cores": {"value": round(vn * 8 / 1e9, 3), "mvalues_per_s": round(vn / 1e6, 1), "cores": cores,
+                              "rows_read": dn, "seconds": round(en, 2)}}
+    finally:
+        os.unlink(path)
+
+
 def load_traffic():
     """Per-launch HBM bytes from the committed rocprofv3 --pmc summary, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_rlev2_decode.json")
@@ -475,6 +534,7 @@ def main():
             line["copy_inclusive"] = copy_incl
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(data, N, args.cpu_budget)
+            line["cpu_baseline"]["reference_pyarrow"] = pyarrow_baseline(values, args.cpu_budget)
         print(json.dumps(line), flush=True)
     if dist:
         dist.barrier()

@@ -288,6 +288,15 @@ int orcg_dict_gather_device(orcg_ctx* ctx, const void* d_indices, int index_widt
  * Decimal64ColumnReader". Synchronous. */
 int orcg_decimal_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len, const int64_t* d_scales,
                                uint64_t nvalues, uint32_t precision, int32_t scale, void* d_out);
+/* Hive 0.11 decimals (precision 0) under RowReaderOptions::
+ * throwOnHive11DecimalOverflow (c++/include/orc/Reader.hh:258-271;
+ * DecimalHive11ColumnReader::next, c++/src/ColumnReader.cc:1638-1680): 1 is
+ * orcg_decimal_decode_device(precision 0); 0 replaces every value past 128
+ * bits or 38 digits by NULL instead of raising: d_keep[k] (nvalues bytes) is 0
+ * for such a value (its slot holds 0) and 1 otherwise. Synchronous. */
+int orcg_hive11_decimal_decode_device(orcg_ctx* ctx, const uint8_t* d_src, uint64_t src_len, const int64_t* d_scales,
+                                      uint64_t nvalues, int32_t scale, int throw_on_overflow, void* d_out,
+                                      uint8_t* d_keep);
 /* TimestampColumnReader::next value construction (c++/src/ColumnReader.cc
  * :318-347) in place: seconds += epoch (1420070400 for UTC writers), nanos
  * from the trailing-zero code; writer and reader zones with equal rules. */

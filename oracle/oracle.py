@@ -59,6 +59,7 @@ def lib():
             ("orco_dict_offsets", [vp, u64, vp], None),
             ("orco_dict_gather", [vp, u64, vp, vp, u64, vp, vp], i32),
             ("orco_decimal_decode", [vp, sz, vp, u64, i32, i32, vp], i32),
+            ("orco_decimal_decode_keep", [vp, sz, vp, u64, i32, vp, vp], i32),
             ("orco_timestamp", [vp, vp, u64, ctypes.c_int64], None),
         ]:
             f = getattr(L, name)
@@ -206,6 +207,21 @@ def decimal_decode(data, scales, n, scale, wide):
                              out.ctypes.data) != 0:
         raise OracleError(L.orco_last_error().decode())
     return out
+
+
+def decimal_decode_keep(data, scales, n, scale):
+    """Hive 0.11 decimals with throwOnHive11DecimalOverflow(false)
+    (orco_decimal_decode_keep): ([hi, lo] int64[n, 2], keep uint8[n]); an
+    overflowing value reads 0 with keep 0."""
+    L = lib()
+    buf = np.frombuffer(bytes(data), dtype=np.uint8)
+    sc = np.ascontiguousarray(scales, dtype=np.int64)
+    out = np.zeros((n, 2), dtype=np.int64)
+    keep = np.zeros(n, dtype=np.uint8)
+    if L.orco_decimal_decode_keep(buf.ctypes.data, buf.size, sc.ctypes.data, n, int(scale), out.ctypes.data,
+                                  keep.ctypes.data) != 0:
+        raise OracleError(L.orco_last_error().decode())
+    return out, keep
 
 
 def timestamp(secs, nanos, epoch=1420070400):

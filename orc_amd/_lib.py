@@ -95,6 +95,7 @@ SIGNATURES = [
     ("orcg_dict_offsets_device", [vp, vp, u64, vp], i32),
     ("orcg_dict_gather_device", [vp, vp, i32, vp, u64, vp, u64, vp, vp], i32),
     ("orcg_decimal_decode_device", [vp, vp, u64, vp, u64, ctypes.c_uint32, i32, vp], i32),
+    ("orcg_hive11_decimal_decode_device", [vp, vp, u64, vp, u64, i32, i32, vp, vp], i32),
     ("orcg_timestamp_decode_device", [vp, vp, vp, u64, ctypes.c_int64], i32),
     ("orcg_decode_integer_column", [vp, vp, u64, vp, u64, i32, u64, vp, vp], i32),
     ("orcg_java_last_error", [], cp),

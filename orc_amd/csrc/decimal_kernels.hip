@@ -125,12 +125,16 @@ __device__ __forceinline__ U128 div128_pow10(U128 v, uint32_t k) {
 // pairs = orc::Int128's layout, readInt128); 2: Hive 0.11 decimals (precision
 // 0, DecimalHive11ColumnReader::readInt128, ColumnReader.cc:1586-1617): as 1,
 // plus the 128-bit varint limit and the 38-digit range check, both reported
-// as "Hive 0.11 decimal was more than 38 digits." (throwOnHive11DecimalOverflow)
+// as "Hive 0.11 decimal was more than 38 digits." (throwOnHive11DecimalOverflow);
+// 3: as 2 with throwOnHive11DecimalOverflow(false): such a value becomes NULL
+// (keep[k] = 0, value 0; :1646-1677), every other keep[k] = 1.
 template <int kMode>
 __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
     const uint8_t* __restrict__ src, uint64_t len, const int64_t* __restrict__ tile_base,
     const int64_t* __restrict__ scales, uint64_t nvalues, int32_t col_scale, void* __restrict__ out,
-    unsigned long long* err) {
+    unsigned long long* err, uint8_t* __restrict__ keep) {
+  constexpr bool kHive = kMode >= 2;
+  __shared__ uint8_t s_bad[kMode == 3 ? kVTile : 1];  // mode 3: the varint ran past 128 bits
   __shared__ uint32_t s_buf[(kLook + kVTile) / 4 + 1];
   __shared__ uint32_t s_wsum[kVThreads / 64];
   // the tile's varints, by rank: unscaled values (Decimal64: zigzag-decoded
@@ -188,7 +192,7 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
     bool too_long = false;  // kMode 2: more than 128 bits (:1600)
     auto push = [&](uint32_t b) {
       const uint64_t x = b & 0x7fu;
-      if constexpr (kMode == 2) too_long = too_long || shift > 128 || (shift == 126 && x > 3);
+      if constexpr (kHive) too_long = too_long || shift > 128 || (shift == 126 && x > 3);
       if constexpr (kMode == 0) {
         acc_lo |= x << (shift & 63u);  // x86 shift-count masking of readInt64's UB shift
       } else {
@@ -232,6 +236,7 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
           s_hi[r] = acc_hi;
           if constexpr (kMode == 2)
             if (too_long && kt + r < nvalues) atomicMin(err, (unsigned long long)(((kt + r) << 8) | kErrHive11Overflow));
+          if constexpr (kMode == 3) s_bad[r] = too_long ? 1 : 0;
         }
         ++r;
         acc_lo = acc_hi = 0;
@@ -283,12 +288,18 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
           c -= a;
         }
       }
-      if constexpr (kMode == 2) {
+      if constexpr (kHive) {
         // value >= MIN_VALUE && value <= MAX_VALUE, |v| <= 10^38 - 1 (:1616)
         const U128 m = (int64_t)v.hi < 0 ? neg128(v) : v;
         const uint64_t kHi = 0x4B3B4CA85A86C47Aull, kLo = 0x098A223FFFFFFFFFull;
-        if (m.hi > kHi || (m.hi == kHi && m.lo > kLo))
-          atomicMin(err, (unsigned long long)((k << 8) | kErrHive11Overflow));
+        const bool over = m.hi > kHi || (m.hi == kHi && m.lo > kLo);
+        if constexpr (kMode == 2) {
+          if (over) atomicMin(err, (unsigned long long)((k << 8) | kErrHive11Overflow));
+        } else {
+          const bool null_it = over || s_bad[i];
+          keep[k] = null_it ? 0 : 1;
+          if (null_it) v = U128{0, 0};
+        }
       }
       int64_t* o = (int64_t*)out + 2 * k;
       o[0] = (int64_t)v.hi;
@@ -326,18 +337,24 @@ int launch_varint_tile_counts(Ctx* ctx, const uint8_t* d_src, uint64_t len, int6
 }
 
 int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
-                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out) {
+                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out,
+                          uint8_t* d_keep) {
   const uint64_t ntiles = (len + kVTile - 1) / kVTile;
   if (ntiles == 0 || nvalues == 0) return ORCG_OK;
-  if (mode == 2)
-    hipLaunchKernelGGL(varint_decimal_kernel<2>, dim3((unsigned)ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
-                       d_tile_base, d_scales, nvalues, scale, d_out, ctx->d_err);
+  if (mode == 3 && !d_keep) return set_error(ctx, ORCG_INVALID_ARGUMENT, "mode 3 needs a keep array");
+  const dim3 grid((unsigned)ntiles), block(kVThreads);
+  if (mode == 3)
+    hipLaunchKernelGGL(varint_decimal_kernel<3>, grid, block, 0, ctx->stream, d_src, len, d_tile_base, d_scales,
+                       nvalues, scale, d_out, ctx->d_err, d_keep);
+  else if (mode == 2)
+    hipLaunchKernelGGL(varint_decimal_kernel<2>, grid, block, 0, ctx->stream, d_src, len, d_tile_base, d_scales,
+                       nvalues, scale, d_out, ctx->d_err, d_keep);
   else if (mode == 1)
-    hipLaunchKernelGGL(varint_decimal_kernel<1>, dim3((unsigned)ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
-                       d_tile_base, d_scales, nvalues, scale, d_out, ctx->d_err);
+    hipLaunchKernelGGL(varint_decimal_kernel<1>, grid, block, 0, ctx->stream, d_src, len, d_tile_base, d_scales,
+                       nvalues, scale, d_out, ctx->d_err, d_keep);
   else
-    hipLaunchKernelGGL(varint_decimal_kernel<0>, dim3((unsigned)ntiles), dim3(kVThreads), 0, ctx->stream, d_src, len,
-                       d_tile_base, d_scales, nvalues, scale, d_out, ctx->d_err);
+    hipLaunchKernelGGL(varint_decimal_kernel<0>, grid, block, 0, ctx->stream, d_src, len, d_tile_base, d_scales,
+                       nvalues, scale, d_out, ctx->d_err, d_keep);
   return hip_check(ctx, hipGetLastError(), "varint_decimal_kernel launch");
 }
 

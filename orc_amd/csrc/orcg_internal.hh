@@ -125,8 +125,11 @@ int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t
 // int64 (Decimal64) or [hi, lo] int64 pairs (Decimal128, orc::Int128 layout).
 int launch_varint_tile_counts(Ctx* ctx, const uint8_t* d_src, uint64_t len, int64_t* d_counts, uint64_t* ntiles);
 constexpr uint64_t kVarintTile = 4096;
+// mode: 0 Decimal64, 1 Decimal128, 2 Hive 0.11 (overflow raises), 3 Hive 0.11
+// with overflowing values nulled (d_keep[k] = 0; 1 otherwise)
 int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
-                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out);  // mode: 0 Decimal64, 1 Decimal128, 2 Hive 0.11
+                          const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out,
+                          uint8_t* d_keep = nullptr);
 // TimestampColumnReader value construction, in place.
 int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, int64_t epoch);
 

@@ -265,6 +265,7 @@ struct orcg_reader {
   bool decimal_as_long = false;  // PostScript version 1.9999 (UNSTABLE-PRE-2.0): Decimal64V2 columns (Reader.cc:1693-1699)
   bool lazy_dict = false;
   int32_t hive11_scale = 6;  // RowReaderOptions::forcedScaleOnHive11Decimal (Reader.cc RowReaderOptionsPrivate: 6)
+  bool hive11_throw = true;  // RowReaderOptions::throwOnHive11DecimalOverflow (default true)
   std::string software_version;  // orcg_reader_software_version's buffer  // RowReaderOptions::setEnableLazyDecoding: dictionary columns keep index + dictionary only
   std::vector<std::unique_ptr<DevSlot>> slots;  // results of the last read, in stripe order
   size_t nslots = 0;
@@ -633,8 +634,13 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
                                 : ORCG_OK;
       });
       ORCG_ALLOC(int64_t, dense, wide ? 2 * nonnull : nonnull);
+      // throwOnHive11DecimalOverflow(false): overflowing values become NULL
+      const bool nullify = hive11 && !hive11_throw;
+      uint8_t* keep = nullptr;
+      if (nullify) ORCG_ALLOC_TO(uint8_t, keep, nonnull + 8);
       if ((rc = launch_varint_decimal(ctx, d_src, sb.len, base, scales, nonnull,
-                                    hive11 ? hive11_scale : (int32_t)t.scale, hive11 ? 2 : (wide ? 1 : 0), dense)))
+                                    hive11 ? hive11_scale : (int32_t)t.scale,
+                                    hive11 ? (nullify ? 3 : 2) : (wide ? 1 : 0), dense, keep)))
         return fail_ctx(rc);
       if (!row_nn) {
         c.data = dense;
@@ -642,6 +648,26 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
         ORCG_ALLOC(int64_t, out, wide ? 2 * n : n);
         if ((rc = scatter(dense, row_nn, n, out, wide ? 16 : 8))) return fail_ctx(rc);
         c.data = out;
+      }
+      if (nullify && nonnull) {
+        // the row mask: rows present in the stream AND kept (the reference
+        // clears notNull[i] and sets hasNulls, ColumnReader.cc:1650-1677)
+        uint8_t* rnn = keep;
+        if (row_nn) {
+          ORCG_ALLOC_TO(uint8_t, rnn, n + 8);
+          if ((rc = scatter(keep, row_nn, n, rnn, 1))) return fail_ctx(rc);
+        }
+        if ((rc = launch_count_nonzero(ctx, rnn, n, D->d_scalars + 3))) return fail_ctx(rc);
+        const uint64_t* kept = defer(D->d_scalars + 3, 1);
+        if (!kept) return fail(ORCG_DEVICE_ERROR, "D2H of the kept decimal count failed");
+        Col* cp = &c;
+        checks.push_back([cp, kept, rnn, n]() -> int {
+          if (*kept < n) {
+            cp->has_nulls = true;
+            cp->nn = rnn;
+          }
+          return ORCG_OK;
+        });
       }
     }
   } else if (k == ORCG_TYPE_TIMESTAMP || k == ORCG_TYPE_TIMESTAMP_INSTANT) {
@@ -1674,8 +1700,9 @@ int orcg_reader_set_lazy_dictionary(orcg_reader* r, int on) {
 }
 int orcg_reader_set_hive11_decimal(orcg_reader* r, int32_t forced_scale, int throw_on_overflow) {
   if (!r || forced_scale < 0 || forced_scale > 38) return ORCG_INVALID_ARGUMENT;
-  if (!throw_on_overflow) return r->fail(ORCG_INVALID_ARGUMENT, "throwOnHive11DecimalOverflow(false) is not supported");
+  std::lock_guard<std::mutex> lk(r->mu);
   r->hive11_scale = forced_scale;
+  r->hive11_throw = throw_on_overflow != 0;
   return ORCG_OK;
 }
 int32_t orcg_reader_hive11_scale(const orcg_reader* r) { return r ? r->hive11_scale : 6; }

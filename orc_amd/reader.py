@@ -402,7 +402,8 @@ class Reader:
 
     def set_hive11_decimal(self, forced_scale=6, throw_on_overflow=True):
         """RowReaderOptions::forcedScaleOnHive11Decimal /
-        throwOnHive11DecimalOverflow (only throwing is supported)."""
+        throwOnHive11DecimalOverflow (c++/include/orc/Reader.hh:258-271):
+        with throw_on_overflow=False a value past 38 digits reads as NULL."""
         check(self._L.orcg_reader_set_hive11_decimal(self._h, int(forced_scale), int(bool(throw_on_overflow))),
               self._err)
 

@@ -88,6 +88,9 @@ def main():
          "Hive 0.11 decimal was more than 38 digits."),
         ("testDecimalHive11OverflowExceptionNull", 6, "presentBuffer", "numBuffer", [0],
          "Hive 0.11 decimal was more than 38 digits."),
+        # throwOnHive11DecimalOverflow(false): the two overflowing values of
+        # the four non-null rows are replaced by NULL (None), the others read 1
+        ("testDecimalHive11OverflowNull", 6, "presentBuffer", "numBuffer", [None, 1, None, 1], None),
     ]
     for name, forced, pres, num, expected, err in hive:
         line, body = blk(name)
@@ -100,6 +103,8 @@ def main():
         }
         if err:
             fx["error"] = err
+        if name == "testDecimalHive11OverflowNull":
+            fx["throw_on_overflow"] = False
         out.append(fx)
     line, body = blk("testTimestamp", "TestColumnReader")
     dates = re.findall(r'"(\w{3} \w{3} [ \d]\d \d\d:\d\d:\d\d \d{4})\\n"', body)

@@ -56,6 +56,24 @@ def _device_decimal(data, scales, n, precision, scale):
     return out.cpu().numpy()
 
 
+def _device_hive11_keep(data, scales, n, scale):
+    """orcg_hive11_decimal_decode_device with throw_on_overflow = 0."""
+    import torch
+
+    import orc_amd
+
+    ctx = orc_amd.default_context(0)
+    L = orc_amd._lib.load()
+    d_src = torch.frombuffer(bytearray(data) or bytearray(1), dtype=torch.uint8).cuda()
+    d_sc = torch.from_numpy(np.ascontiguousarray(scales, dtype=np.int64)).cuda()
+    out = torch.full((n, 2), 7, dtype=torch.int64, device="cuda")
+    keep = torch.full((n,), 9, dtype=torch.uint8, device="cuda")
+    ctx.after_torch()
+    orc_amd._lib.check(L.orcg_hive11_decimal_decode_device(ctx.handle, d_src.data_ptr(), len(data), d_sc.data_ptr(), n,
+                                                           scale, 0, out.data_ptr(), keep.data_ptr()), ctx.last_error)
+    return out.cpu().numpy(), keep.cpu().numpy()
+
+
 @pytest.mark.parametrize("fx", DECIMAL, ids=[f["name"] for f in DECIMAL])
 def test_decimal_timestamp_kat_on_device(fx):
     import torch
@@ -70,6 +88,13 @@ def test_decimal_timestamp_kat_on_device(fx):
         if fx.get("error"):  # Hive 0.11 overflow (throwOnHive11DecimalOverflow)
             with pytest.raises(orc_amd.ParseError, match=fx["error"]):
                 _device_decimal(data, scales, n, fx["precision"], fx["scale"])
+            return
+        if fx.get("throw_on_overflow") is False:  # overflowing values -> NULL
+            got, keep = _device_hive11_keep(data, scales, n, fx["scale"])
+            vals = [v if k else None for v, k in zip(_to_int128(got), keep)]
+            assert vals == fx["expected"]
+            with pytest.raises(orc_amd.ParseError, match="more than 38 digits"):
+                _device_decimal(data, scales, n, 0, fx["scale"])
             return
         got = _device_decimal(data, scales, n, fx["precision"], fx["scale"])
         vals = _to_int128(got) if fx["precision"] > 18 or fx["precision"] == 0 else [int(v) for v in got]
@@ -240,3 +265,18 @@ def test_pyarrow_written_decimals_and_timestamps(tmp_path):
         gt = g["t"]
         assert (gt is None and want_ns[i] is None) or int(gt.astype(np.int64)) == want_ns[i], i
     assert len(got) == n
+
+
+def test_hive11_file_non_throwing_mode_matches_throwing():
+    """orc-file-11-format.orc (Hive 0.11 decimals) read with
+    throwOnHive11DecimalOverflow(false): no value overflows, so every batch
+    equals the throwing mode's (the nulling path runs and keeps hasNulls as
+    the PRESENT stream has it)."""
+    import orc_amd
+    from file_parity import path
+
+    r = orc_amd.Reader(path("orc-file-11-format.orc"), orc_amd.default_context(0))
+    want = r.read()
+    r.set_hive11_decimal(6, throw_on_overflow=False)
+    got = r.read()
+    assert got == want

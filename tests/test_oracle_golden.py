@@ -122,6 +122,11 @@ def _kat_nonnull(fx):
     return int(np.count_nonzero(dec.next(len(fx["expected"]) * 2 + 64)[: 10 ** 6]))
 
 
+def _i128(h, lo):
+    v = ((int(h) & ((1 << 64) - 1)) << 64) | (int(lo) & ((1 << 64) - 1))
+    return v - (1 << 128) if v >> 127 else v
+
+
 @pytest.mark.parametrize("fx", DECIMAL, ids=[f["name"] for f in DECIMAL])
 def test_decimal_timestamp_kat(fx):
     """Decimal64/128 and timestamp known answers of TestColumnReader.cc: the
@@ -134,6 +139,14 @@ def test_decimal_timestamp_kat(fx):
         wide = 2 if fx["precision"] == 0 else fx["precision"] > 18  # 2: Hive 0.11 (forced scale)
         if fx.get("error"):
             with pytest.raises(oracle.OracleError, match=fx["error"]):
+                oracle.decimal_decode(data, scales, n, fx["scale"], wide)
+            return
+        if fx.get("throw_on_overflow") is False:
+            # throwOnHive11DecimalOverflow(false): overflow -> NULL (None)
+            got, keep = oracle.decimal_decode_keep(data, scales, n, fx["scale"])
+            vals = [_i128(h, lo) if k else None for (h, lo), k in zip(got, keep)]
+            assert vals == fx["expected"]
+            with pytest.raises(oracle.OracleError, match="more than 38 digits"):
                 oracle.decimal_decode(data, scales, n, fx["scale"], wide)
             return
         got = oracle.decimal_decode(data, scales, n, fx["scale"], wide)

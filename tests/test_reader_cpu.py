@@ -143,16 +143,16 @@ def test_metadata_matches_reference_testmatch(d):
 
 def test_hive11_decimal_options():
     """RowReaderOptions::forcedScaleOnHive11Decimal (default 6, Reader.hh:258-271)
-    on a Hive 0.11 file (decimal1 has precision 0); only the throwing overflow
-    mode (the reference's default) is supported. No GPU."""
+    and throwOnHive11DecimalOverflow on a Hive 0.11 file (decimal1 has
+    precision 0). No GPU."""
     r = orc_amd.Reader(path("orc-file-11-format.orc"))
     dec = [t for t in r.types if t.kind == 14]
     assert dec and all(t.precision == 0 for t in dec)
     assert r.hive11_scale == 6
     r.set_hive11_decimal(3)
     assert r.hive11_scale == 3
-    with pytest.raises(orc_amd.OrcError):
-        r.set_hive11_decimal(6, throw_on_overflow=False)
+    r.set_hive11_decimal(4, throw_on_overflow=False)
+    assert r.hive11_scale == 4
     with pytest.raises(orc_amd.OrcError):
         r.set_hive11_decimal(39)
-    assert r.hive11_scale == 3
+    assert r.hive11_scale == 4
