@@ -51,7 +51,7 @@ struct Ctx {
   int rlev2_variant = ORCG_RLEV2_TILED;  // which RLEv2 kernel to launch
   void* d_defer = nullptr;  // RLEv2 short-run segment queue (rlev2_tiled.hip defer_queue)
   uint64_t defer_cap = 0;
-  uint64_t defer_seq = 0;  // launches that used the queue (count parity)
+  uint64_t defer_seq = 0;  // serial + drain launch pairs so far (their entries' stamps)
   int num_cus = 0;         // compute units of `device` (0 = not queried yet)
   // job tables of multi-stream RLEv2 launches: a pinned host ring and its
   // device mirror (launch_rlev2_multi)
@@ -96,7 +96,7 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
 
 // RLEv2 kernel variants a context accepts (orcg_rlev2_variants): 0 default,
 // 1 wave-walk, and pins of single tiled instances (launch_rlev2_tiled).
-constexpr int kMaxRlev2Variant = 27;
+constexpr int kMaxRlev2Variant = 30;
 bool rlev2_variant_valid(int v);
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,

@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cstdio>
 #include <chrono>
 #include <condition_variable>
 #include <cstring>
@@ -130,7 +131,11 @@ struct DevPool {
       // drop cached blocks and retry once
       for (auto& kv : free_blocks) (void)hipFree(kv.second);
       free_blocks.clear();
-      if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        static const bool dbg = getenv("ORCG_DEBUG_ALLOC") != nullptr;
+        if (dbg) fprintf(stderr, "orcg: device allocation of %zu bytes failed\n", bytes);
+        return nullptr;
+      }
     }
     used.emplace_back(p, bytes);
     return p;

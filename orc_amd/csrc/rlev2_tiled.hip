@@ -91,6 +91,7 @@ constexpr int kOptT4 = 32;
 constexpr int kOptD3 = 64;      // dense discovery: predicated chain marks, wave-reduced control atomics, inline probe
 constexpr int kOptDirect = 128; // dense expansion: lanes store their short runs' values straight to the output (no stage)
 constexpr int kOptPair = 256;   // full DIRECT runs: two values per lane, one 16-byte store (16-byte aligned int64 output)
+constexpr int kOptVP = 512;     // serial groups of short runs expanded value-parallel (coalesced stores)
 
 // Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
 // counts the values of the runs it expands; each pass checks the count
@@ -758,6 +759,63 @@ __device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_
   }
 }
 
+// Expand runs [r0, r1) (<= 64 short SHORT_REPEAT / DIRECT / fixed-delta runs)
+// value-parallel: lane k parses run r0 + k, a wave scan of the run lengths
+// gives each run's first value in the group, then lane t of every 64-value
+// chunk finds its run by a binary search over the lanes (ds_bpermute) and
+// extracts its value, so each store instruction writes 64 consecutive values
+// (one lane per run scatters every store over up to 64 cache lines). Returns
+// false, having done nothing, when the group holds a run it does not handle
+// (PATCHED_BASE, variable-width DELTA).
+template <int kOpt, typename T, typename OffT>
+__device__ __forceinline__ bool group_expand_vp(const uint32_t* win, const OffT* s_off, const uint32_t* s_val,
+                                                uint32_t r0, uint32_t r1, uint64_t vi, int is_signed,
+                                                uint64_t value_begin, uint64_t value_end, T* dst, int lane) {
+  const uint32_t n = r1 - r0;
+  const uint32_t r = r0 + (uint32_t)lane;
+  const bool act = r < r1;
+  const uint32_t hoff = act ? s_off[r] : s_off[r0];
+  const Run run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
+  if (__ballot(act && (run.kind == 2 || (run.kind == 3 && run.W != 0))) != 0) return false;
+  ORCG_COVER_ADD(act ? run.L : 0u);
+  const uint32_t L = act ? run.L : 0u;
+  const uint32_t incl = wave_scan_u32(L);
+  const uint32_t st = incl - L;  // the run's first value in the group
+  const uint32_t total = rdlane(incl, 63);
+  const uint32_t kw = act ? (run.kind | (run.W << 8)) : 0u;
+  const uint32_t db = hoff + run.data;
+  const uint64_t o0 = vi + uni(s_val[r0]);
+  auto perm = [](uint32_t v, uint32_t src) -> uint32_t {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+  };
+  for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
+    const uint32_t t = t0 + (uint32_t)lane;
+    // the last run whose first value is <= t (runs of >= 1 value: it holds t)
+    uint32_t k = 0;
+#pragma unroll
+    for (uint32_t step = 32; step >= 1; step >>= 1)
+      if (k + step < n && perm(st, k + step) <= t) k += step;
+    const uint32_t kwk = perm(kw, k), kind = kwk & 0xffu, W = kwk >> 8;
+    const uint32_t j = t - perm(st, k);
+    const uint64_t a = ((uint64_t)perm((uint32_t)(run.a >> 32), k) << 32) | perm((uint32_t)run.a, k);
+    uint64_t v;
+    if (kind == 1) {
+      const uint32_t bit = j * W;
+      const uint32_t br = perm(db, k) + (bit >> 3);
+      v = field(lds12(win, br), br, bit & 7u, W);
+      if (is_signed) v = unzigzag(v);
+    } else if (kind == 3) {
+      const uint64_t b = ((uint64_t)perm((uint32_t)(run.b >> 32), k) << 32) | perm((uint32_t)run.b, k);
+      v = a + (uint64_t)j * b;
+    } else {
+      v = a;
+    }
+    const uint64_t o = o0 + t;
+    if (t < total && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), v);
+  }
+  return true;
+}
+
 // ---- dense mode -----------------------------------------------------------
 
 struct DenseResult {
@@ -1384,13 +1442,14 @@ __device__ __forceinline__ uint32_t* s_dense_mark(DenseLds<kDense>& d) {
 }
 
 // Deferral (kDefer): a serial-walk instance (kDefer = 1) whose probe pass
-// finds short runs stops at the end of that pass and queues {segment, byte
-// offset, value index} in `defer_q` (two counts, two cursors, then 3 words per entry);
-// the dense instance launched right after it (kDefer = 2) drains the queue
-// with a persistent grid, so a short-run segment never runs the one-wave
-// header walk, whatever the stream's overall density. Launches alternate
-// between the two counts (`defer_par`): the drain of launch k zeroes the
-// count launch k + 1 will use, one store instead of a grid-wide handshake.
+// finds short runs stops at the end of that pass and records {stamp, byte
+// offset, value index} in the segment's own entry of `defer_q` (3 words per
+// launch-wide segment; stamp = the launch pair's sequence number
+// `defer_par`); the dense instance launched right after it (kDefer = 2)
+// decodes the stamped segments with a persistent grid, each workgroup a
+// static share, so a short-run segment never runs the one-wave header walk,
+// whatever the stream's overall density. Entries of older launches carry
+// older stamps: nothing is ever reset.
 template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMinWaves, int kDense = 0, int kDefer = 0,
           bool kMulti = false>
 __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
@@ -1713,7 +1772,9 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               // coalesced stores through the wave's value stage
               dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], s_stage2 + wave * kStage, r0, e, vi,
                                  is_signed, value_begin, value_end, dst, lane);
-            else
+            else if (!((kOpt & kOptVP) != 0 &&
+                       group_expand_vp<kOpt>(s_win[0], s_off[0], s_val[0], r0, e, vi, is_signed, value_begin,
+                                             value_end, dst, lane)))
               group_expand<kOpt>(s_win[0], s_off[0], s_val[0], r0, e, vi, is_signed, value_begin, value_end, dst,
                                  lane);
           }
@@ -1745,10 +1806,13 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           // a short-run segment: queue the rest for the dense instance
           if (shrt && pos < seg_end && vi < value_end) {
             if (tid == 0) {
-              const unsigned long long slot = atomicAdd(&defer_q[defer_par], 1ull);
-              defer_q[4 + 3 * slot] = gg;
-              defer_q[5 + 3 * slot] = pos;
-              defer_q[6 + 3 * slot] = vi;
+              // the segment's own entry, stamped with this launch pair's
+              // sequence number (no shared counter: one atomic per queued
+              // segment on one word serialised whole launches)
+              defer_q[3 * gg + 1] = pos;
+              defer_q[3 * gg + 2] = vi;
+              __hip_atomic_store(&defer_q[3 * gg], (unsigned long long)defer_par, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
             }
             return;
           }
@@ -1817,23 +1881,29 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   };
 
   if constexpr (kDefer == 2) {
-    // persistent drain of the queue, entries claimed one at a time (their
-    // costs differ); the next launch's count and cursor start at 0
-    __shared__ unsigned long long s_next;
-    if (blockIdx.x == 0 && tid == 0) {
-      defer_q[defer_par ^ 1u] = 0;
-      defer_q[2 + (defer_par ^ 1u)] = 0;
-    }
-    const uint64_t count = uni64(defer_q[defer_par]);
-    // the first entry by workgroup index, the rest from the cursor (no
-    // atomics at all when the queue is short or empty)
-    for (uint64_t i = blockIdx.x; i < count;) {
-      run_segment(uni64(defer_q[4 + 3 * i]), true, uni64(defer_q[5 + 3 * i]), uni64(defer_q[6 + 3 * i]));
-      if (gridDim.x >= count) break;
-      __syncthreads();  // LDS (and s_next) are reused by the next entry
-      if (tid == 0) s_next = gridDim.x + atomicAdd(&defer_q[2 + defer_par], 1ull);
+    // the drain: workgroup w takes the contiguous share [w C, (w + 1) C) of
+    // the launch's segments, finds the ones the serial launch stamped with
+    // this pair's sequence number (one stamp load per thread, a ballot per
+    // wave: an empty share costs one load round) and decodes the rest of
+    // each (no counters)
+    __shared__ unsigned long long s_flags[kWaves];
+    const uint64_t per = (p_nsegs + gridDim.x - 1) / gridDim.x;
+    const uint64_t g0 = (uint64_t)blockIdx.x * per;
+    const uint64_t g1 = min(g0 + per, p_nsegs);
+    for (uint64_t b = g0; b < g1; b += kThreads) {
+      const uint64_t g = b + (uint64_t)tid;
+      const bool mine = g < g1 && defer_q[3 * g] == (unsigned long long)defer_par;
+      const unsigned long long m = __ballot(mine);
+      if (lane == 0) s_flags[wave] = m;
       __syncthreads();
-      i = uni64(s_next);
+      for (int w = 0; w < kWaves; ++w) {
+        for (unsigned long long f = uni64(s_flags[w]); f; f &= f - 1) {
+          const uint64_t q = b + (uint64_t)(w * kWave + __builtin_ctzll(f));
+          run_segment(q, true, uni64(defer_q[3 * q + 1]), uni64(defer_q[3 * q + 2]));
+          __syncthreads();  // LDS is reused by the next segment
+        }
+      }
+      __syncthreads();  // s_flags is rewritten by the next round
     }
   } else {
     run_segment(blockIdx.x, false, 0, 0);
@@ -1856,9 +1926,8 @@ bool rlev2_variant_valid(int v) {
 }
 
 static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
-  // [0], [1] entry counts and [2], [3] drain cursors of even / odd launches,
-  // then {segment, byte offset, value index} per entry; all start at zero;
-  // each drain zeroes the count and cursor of the next launch
+  // {stamp, byte offset, value index} per launch-wide segment, stamps zeroed
+  // at allocation (launch sequence numbers start at 1)
   if (ctx->defer_cap < nsegs) {
     if (ctx->d_defer) {
       (void)hipStreamSynchronize(ctx->stream);
@@ -1866,9 +1935,9 @@ static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
       ctx->d_defer = nullptr;
       ctx->defer_cap = 0;
     }
-    const uint64_t cap = std::max<uint64_t>(nsegs, 4096);
-    int rc = hip_check(ctx, hipMalloc(&ctx->d_defer, (4 + 3 * cap) * 8), "hipMalloc defer queue");
-    if (!rc) rc = hip_check(ctx, hipMemsetAsync(ctx->d_defer, 0, 32, ctx->stream), "defer queue reset");
+    const uint64_t cap = std::max<uint64_t>(nsegs + nsegs / 4, 4096);
+    int rc = hip_check(ctx, hipMalloc(&ctx->d_defer, 3 * cap * 8), "hipMalloc defer queue");
+    if (!rc) rc = hip_check(ctx, hipMemsetAsync(ctx->d_defer, 0, 3 * cap * 8, ctx->stream), "defer queue reset");
     if (rc) return rc;
     ctx->defer_cap = cap;
   }
@@ -1968,7 +2037,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
   do {                                                                              \
     int rc_ = defer_queue(ctx, nsegs, &dq);                                          \
     if (rc_) return rc_;                                                            \
-    dpar = (uint32_t)(ctx->defer_seq++ & 1u);                                       \
+    dpar = (uint32_t)(ctx->defer_seq++ % 0xffffffffull) + 1u; /* never 0 */         \
     ORCG_KX(O, WKB, false, MWV, 0, 1, (unsigned)nsegs);                              \
     ORCG_KX(DO, 8, false, 6, 2, 2, drain);                                           \
   } while (0)
@@ -2001,6 +2070,9 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     case 25: ORCG_KT(kWide | kOptPair, 33, false, 1, false); break;                    // 20 + 16-byte pair stores
     case 26: ORCG_DEFERRING(kWide | kOptD3 | kOptPair, 33, 1, kSer | kOptD3 | kOptPair); break;  // 2 + pair stores
     case 27: ORCG_KT(kSer | kOptPair, 21, false, 6, false); break;                     // 16 + pair stores
+    case 28: ORCG_KT(kWide | kOptPair | kOptVP, 33, false, 1, false); break;           // 25 + value-parallel groups
+    case 29: ORCG_KT(kSer | kOptPair | kOptVP, 21, false, 6, false); break;            // 27 + value-parallel groups
+    case 30: ORCG_DEFERRING(kSer | kOptD3 | kOptVP, 21, 6, kSer | kOptD3); break;     // 3 + value-parallel groups
 #endif
     default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "unknown RLEv2 kernel variant");
   }

@@ -75,6 +75,8 @@ for s in $STEPS; do
     proffile)
       export TMPDIR=/tmp
       for w in ${PF_WORKLOADS:-c5}; do run prof_$w 600 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_$w" -o run --output-format csv -- python3 scripts/bench_file.py --workload $w --iters 1 --no-cpu-baseline; done ;;
+    dbg11) run dbg11 300 python scripts/dbg_file11.py ;;
+    treader) run treader 600 python -u -m pytest tests/test_gpu_reader.py -m gpu -q -rf -x --timeout 120 --timeout-method thread ;;
     benchwalk) run bench_walk 600 python bench.py --variant 1 --no-cpu-baseline ;;
     prof)
       export TMPDIR=/tmp
