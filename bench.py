@@ -18,6 +18,12 @@ is measured both ways SURVEY.md §8(e) names: every rank D2H's its rows into
 its own slice of one shared host batch (no collective), and an RCCL
 point-to-point gather of the device columns to rank 0 over xGMI.
 
+Before the W warm-up steps, `--settle-ms` (default 60) of back-to-back
+decodes take the GPU out of its idle power state: after the host-side stream
+generation the first ~100 launches run 5-7 % slow (scripts/ramp_probe.py,
+DESIGN.md §4). The JSON line reports them as `settle`; `--settle-ms 0` turns
+them off.
+
 The JSON line also carries
   roofline     achieved algorithmic bytes (S + 8N per launch) / the kernel's
                HIP-event duration on its own stream, vs 8 TB/s HBM3E peak;
@@ -324,15 +330,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    # 100 warm-up launches (~30 ms): after the ~1 s idle of the verification
-    # the clocks need that long to ramp; 10 left the first timed launches
-    # ~4 % slow (measured 0.300 vs 0.289 ms per launch)
-    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--stride", type=int, default=10_000)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--settle-ms", type=float, default=60.0,
+                    help="decode launches before the warm-up until this much GPU time has passed: the GPU leaves "
+                         "its idle power state (the first ~100 launches after an idle second run 5-7 %% slow, "
+                         "DESIGN.md §4); reported in the JSON line as `settle`; 0 = none")
     ap.add_argument("--variant", type=int, default=0, help="RLEv2 kernel variant (0 default, 1 wave-walk, ...)")
     ap.add_argument("--copy-inclusive", type=int, default=3,
                     help="steps of the PCIe-inclusive pipeline to time (host bytes -> host values); 0 = skip")
@@ -403,6 +410,22 @@ def main():
         del d_want
         if not ok:
             raise SystemExit("decode mismatch on rank %d" % rank)
+    # settle: back-to-back decodes until --settle-ms of GPU time has passed
+    # (measured on the decode stream), then the W warm-up steps proper
+    settle = {"launches": 0, "ms": 0.0}
+    if args.settle_ms > 0:
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record(stream)
+        while True:
+            for _ in range(10):
+                step()
+            settle["launches"] += 10
+            s1.record(stream)
+            s1.synchronize()
+            settle["ms"] = round(s0.elapsed_time(s1), 2)
+            if settle["ms"] >= args.settle_ms or settle["launches"] >= 2000:
+                break
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
@@ -497,6 +520,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": settle,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",

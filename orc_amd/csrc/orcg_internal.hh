@@ -79,6 +79,7 @@ struct RleJob {
   uint64_t seg_base;
   uint32_t is_signed;
   uint32_t pad;
+  unsigned long long* err;  // the job's device error record (the reader's per-column word), or null = the launch's
 };
 
 int set_error(Ctx* ctx, int status, const std::string& msg);

@@ -128,6 +128,7 @@ struct DevPool {
     }
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();  // the failure must not stick to a later launch check
       // drop cached blocks and retry once
       for (auto& kv : free_blocks) (void)hipFree(kv.second);
       free_blocks.clear();
@@ -251,6 +252,7 @@ struct DevSlot {
   DevPool pool;
   uint8_t* d_stage = nullptr;
   uint64_t* d_scalars = nullptr;
+  unsigned long long* d_errs = nullptr;  // device error record per column (the kernels' atomicMin word)
   std::vector<ColOut> out;
 };
 
@@ -288,7 +290,13 @@ struct orcg_reader {
   // instead of a synchronisation each. The reference makes them inline.
   uint64_t* h_defer = nullptr;
   size_t defer_cap = 0, defer_used = 0;
-  std::vector<std::function<int()>> checks;
+  // (column, check): run in column order with the columns' device errors
+  std::vector<std::pair<uint32_t, std::function<int()>>> checks;
+  // the column decode() is working on, and the column of the first inline
+  // (host-detected) failure of this stripe
+  static constexpr uint32_t kNoCol = 0xffffffffu;
+  uint32_t cur_col = kNoCol, err_col = kNoCol;
+  int first_error(int inline_rc);
   const uint64_t* defer(const void* d_src, size_t count) {
     if (defer_used + count > defer_cap) return nullptr;
     uint64_t* h = h_defer + defer_used;
@@ -303,11 +311,17 @@ struct orcg_reader {
     if (h_defer) (void)hipHostFree(h_defer);
   }
   int fail(int status, const std::string& m) {
+    if (err_col == kNoCol) err_col = cur_col;
     last_error = m;
     if (ctx) ctx->last_error = m;
     return status;
   }
   int fail_ctx(int rc) { return fail(rc, ctx ? ctx->last_error : std::string("device error")); }
+  int fail_oom(int line) {
+    static const bool dbg = getenv("ORCG_DEBUG_ALLOC") != nullptr;
+    if (dbg) fprintf(stderr, "orcg: reader device allocation failed at reader_api.cpp:%d (column %u)\n", line, cur_col);
+    return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  }
 
   int open_tail();
   int prepare(uint64_t s, HostStage& hs) const;
@@ -397,7 +411,9 @@ int orcg_reader::open_tail() {
 int orcg_reader::nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out) {
   int rc = launch_count_nonzero(ctx, nn, n, D->d_scalars);
   if (!rc) rc = hip_check(ctx, hipMemcpyAsync(&out, D->d_scalars, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H count");
-  if (!rc) rc = sync_ctx(ctx);
+  // a stream synchronisation only: the columns' device error records are
+  // read once, at the end of the stripe (first_error)
+  if (!rc) rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
   return rc;
 }
 
@@ -407,10 +423,12 @@ int orcg_reader::scatter(const void* dense, const uint8_t* nn, uint64_t n, void*
 
 #define ORCG_ALLOC(T, v, count)                                                   \
   T* v = alloc<T>(count);                                                         \
-  if (!v) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed")
+  if (!v) return fail_oom(__LINE__)
 #define ORCG_ALLOC_TO(T, v, count)                                                \
-  v = alloc<T>(count);                                                            \
-  if (!v) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed")
+  do {                                                                            \
+    v = alloc<T>(count);                                                          \
+    if (!v) return fail_oom(__LINE__);                                            \
+  } while (0)
 
 // The stream's segment table: the host plan's, or (row-index streams) built
 // on the device from the row groups' positions and the present-row prefix
@@ -449,7 +467,7 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
     return ORCG_OK;
   }
   int64_t* out = alloc<int64_t>(count);
-  if (!out) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  if (!out) return fail_oom(__LINE__);
   *pout = out;
   StreamBuf& sb = c.s[slot];
   if (count == 0) return ORCG_OK;
@@ -496,12 +514,13 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
     j.nsegs = nseg;
   }
   int64_t* out = alloc<int64_t>(count);
-  if (!out) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  if (!out) return fail_oom(__LINE__);
   j.src = D->d_stage + sb.host_off;
   j.src_len = sb.len;
   j.dst = out;
   j.nvalues = count;
   j.is_signed = is_signed ? 1u : 0u;
+  j.err = D->d_errs + id;
   batch.push_back(j);
   batched[(uint64_t)id * 8 + (uint64_t)slot] = {out, count};
   return ORCG_OK;
@@ -566,6 +585,18 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
 int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count, const int64_t* rg_rows) {
   Col& c = H->cols[id];
   if (!selected[id] || !c.supported) return ORCG_OK;
+  // this column's kernels report into its own device error record
+  struct Scope {
+    orcg_reader* r;
+    uint32_t col;
+    unsigned long long* err;
+    ~Scope() {
+      r->cur_col = col;
+      r->ctx->d_err = err;
+    }
+  } scope{this, cur_col, ctx->d_err};
+  cur_col = id;
+  ctx->d_err = D->d_errs + id;
   c.n = n;
   c.decoded = true;
   int rc;
@@ -633,7 +664,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if ((rc = launch_exclusive_scan(ctx, counts, ntiles, base))) return fail_ctx(rc);
       const uint64_t* total = defer(base + ntiles, 1);
       if (!total) return fail(ORCG_DEVICE_ERROR, "D2H of the varint count failed");
-      checks.push_back([this, total, nonnull, cid]() -> int {
+      checks.emplace_back(cur_col, [this, total, nonnull, cid]() -> int {
         return *total < nonnull ? fail(ORCG_PARSE_ERROR, "Read past end of stream in Decimal64ColumnReader column " +
                                                              cid + " kind DATA")
                                 : ORCG_OK;
@@ -642,7 +673,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       // throwOnHive11DecimalOverflow(false): overflowing values become NULL
       const bool nullify = hive11 && !hive11_throw;
       uint8_t* keep = nullptr;
-      if (nullify) ORCG_ALLOC_TO(uint8_t, keep, nonnull + 8);
+      if (nullify) {
+        ORCG_ALLOC_TO(uint8_t, keep, nonnull + 8);
+      }
       if ((rc = launch_varint_decimal(ctx, d_src, sb.len, base, scales, nonnull,
                                     hive11 ? hive11_scale : (int32_t)t.scale,
                                     hive11 ? (nullify ? 3 : 2) : (wide ? 1 : 0), dense, keep)))
@@ -666,7 +699,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
         const uint64_t* kept = defer(D->d_scalars + 3, 1);
         if (!kept) return fail(ORCG_DEVICE_ERROR, "D2H of the kept decimal count failed");
         Col* cp = &c;
-        checks.push_back([cp, kept, rnn, n]() -> int {
+        checks.emplace_back(cur_col, [cp, kept, rnn, n]() -> int {
           if (*kept < n) {
             cp->has_nulls = true;
             cp->nn = rnn;
@@ -746,7 +779,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       Col* cp = &c;
       const bool db_present = db.present;
       const uint64_t db_len = db.present ? db.len : 0;
-      checks.push_back([this, h, cp, db_present, db_len, cid]() -> int {
+      checks.emplace_back(cur_col, [this, h, cp, db_present, db_len, cid]() -> int {
         if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
         if (h[0] > 0 && !db_present)
           return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
@@ -787,7 +820,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       const uint64_t* need = defer(dstart + nonnull, 1);
       if (!need) return fail(ORCG_DEVICE_ERROR, "D2H of the string bytes failed");
       const uint64_t blob_len = c.blob_len;
-      checks.push_back([this, need, blob_len]() -> int {
+      checks.emplace_back(cur_col, [this, need, blob_len]() -> int {
         return *need > blob_len ? fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next") : ORCG_OK;
       });
       if (row_nn) {
@@ -816,7 +849,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     c.offsets = off;
     uint64_t total = 0;
     if ((rc = hip_check(ctx, hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
-        (rc = sync_ctx(ctx)))
+        (rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize")))
       return fail_ctx(rc);
     // the children's row groups start at the list offsets of the parent's
     int64_t* child_rows = nullptr;
@@ -863,7 +896,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     }
     uint64_t first_bad = ~0ull;
     if ((rc = hip_check(ctx, hipMemcpyAsync(&first_bad, bad, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
-        (rc = sync_ctx(ctx)))
+        (rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize")))
       return fail_ctx(rc);
     if (first_bad != ~0ull)
       return fail(ORCG_PARSE_ERROR, "Invalid union tag " + std::to_string(first_bad & 0xff) + " for union with " +
@@ -1188,6 +1221,44 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   return ORCG_OK;
 }
 
+// The stripe's first error, in column order (type ids are pre-order, the
+// order decode() visits the columns): for each column up to the one that
+// failed inline (`inline_rc`, detected on the host while launching), its
+// deferred checks, then its device error record (the first bad value of its
+// kernels), as the reference raises them while reading that column; then the
+// inline failure itself; then the context's own record.
+int orcg_reader::first_error(int inline_rc) {
+  const std::string inline_msg = last_error;
+  const uint32_t inline_col = err_col;
+  cur_col = kNoCol;
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(ORCG_DEVICE_ERROR, "stream synchronize failed");
+  const size_t nc = H->cols.size();
+  std::vector<unsigned long long> rec(nc, kNoError);
+  if (nc && hipMemcpy(rec.data(), D->d_errs, 8 * nc, hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(ORCG_DEVICE_ERROR, "read error records");
+  const uint32_t last = inline_rc ? (inline_col == kNoCol ? 0u : inline_col) : (uint32_t)nc;
+  for (uint32_t col = 0; col < nc && col <= last; ++col) {
+    for (auto& ch : checks)
+      if (ch.first == col) {
+        const int rc = ch.second();
+        if (rc) return rc;
+      }
+    if (rec[col] != kNoError) {
+      const uint32_t code = (uint32_t)(rec[col] & 0xff);
+      ctx->last_error_value = rec[col] >> 8;
+      return fail(dev_error_status(code), dev_error_message(code));
+    }
+  }
+  if (inline_rc) return fail(inline_rc, inline_msg);
+  for (auto& ch : checks)
+    if (ch.first >= nc) {
+      const int rc = ch.second();
+      if (rc) return rc;
+    }
+  const int rc = sync_ctx(ctx);
+  return rc ? fail_ctx(rc) : ORCG_OK;
+}
+
 // Device half: one H2D of the staging buffer, then every selected column.
 int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   const double t0 = now_s();
@@ -1195,9 +1266,11 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   ds.pool.release_all();
   ds.d_stage = (uint8_t*)ds.pool.get(hs.used + 64);
   ds.d_scalars = (uint64_t*)ds.pool.get(64);
-  if (!ds.d_stage || !ds.d_scalars) return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
+  ds.d_errs = (unsigned long long*)ds.pool.get(8 * hs.cols.size() + 8);
+  if (!ds.d_stage || !ds.d_scalars || !ds.d_errs) return fail_oom(__LINE__);
   stage_bytes += hs.used;
   int rc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, hs.used, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
+  if (!rc) rc = hip_check(ctx, hipMemsetAsync(ds.d_errs, 0xff, 8 * hs.cols.size(), ctx->stream), "error records");
   if (!rc) rc = sync_ctx(ctx);
   if (rc) return fail_ctx(rc);
   const double t1 = now_s();
@@ -1214,6 +1287,7 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   }
   defer_used = 0;
   checks.clear();
+  cur_col = err_col = kNoCol;
   batch.clear();
   batched.clear();
   const uint64_t nrows = footer.stripes[hs.stripe].num_rows;
@@ -1227,18 +1301,9 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   }
   if (!rc) rc = decode(0, nrows, nullptr, nrows, rg_rows);
   batched_streams += batch.size();
-  if (rc) (void)hipStreamSynchronize(ctx->stream);  // queued copies land before the buffer is reused
-  if (!rc) {
-    // the checks first (in column order, as the reference raises them), then
-    // the device error record
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess) rc = fail(ORCG_DEVICE_ERROR, "stream synchronize failed");
-    for (auto& ch : checks)
-      if (!rc) rc = ch();
-    if (!rc) {
-      rc = sync_ctx(ctx);
-      if (rc) rc = fail_ctx(rc);
-    }
-  }
+  // queued copies land before the buffer is reused; then the first error in
+  // column order, as the reference raises them one column at a time
+  rc = first_error(rc);
   checks.clear();
   ds.out.assign(hs.cols.size(), ColOut());
   for (size_t i = 0; i < hs.cols.size(); ++i) {

@@ -92,6 +92,8 @@ constexpr int kOptD3 = 64;      // dense discovery: predicated chain marks, wave
 constexpr int kOptDirect = 128; // dense expansion: lanes store their short runs' values straight to the output (no stage)
 constexpr int kOptPair = 256;   // full DIRECT runs: two values per lane, one 16-byte store (16-byte aligned int64 output)
 constexpr int kOptVP = 512;     // serial groups of short runs expanded value-parallel (coalesced stores)
+constexpr int kOptUnion = 1024; // dense v2 instance whose serial (long-run) windows also cover the dense stage and
+                                // marks: one instance routes each window by its runs (dense or serial), no queue
 
 // Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
 // counts the values of the runs it expands; each pass checks the count
@@ -574,7 +576,8 @@ __device__ __forceinline__ void walk_extent(const LaneWin& hw, uint32_t lp, uint
 
 // Wave-uniform header walk over the window [wpos, wpos + kWin): records runs
 // starting at pos.. into (run_off, run_val) until the next run starts past
-// kWin - kMaxRun, leaves the segment, or the table is full. With `pub` the
+// kWin - kMaxRun and does not end inside the loaded bytes (`lim`), leaves the
+// segment, or the table is full. With `pub` the
 // walk also cuts the runs into work items (`items`, ends by run index) and
 // publishes the item count as items close, so expanding waves start early.
 template <uint32_t kWin, uint32_t kCap, bool kT4 = false, typename OffT = uint32_t>
@@ -612,7 +615,11 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
   const uint32_t lim_all = uni(min(min(a_src, a_seg), lim));
   const bool items_on = uni(pub != nullptr ? 1u : 0u) != 0;
   while (lp < a_seg && vr < v_lim && n < cap) {
-    if (lp >= kChunk && n > 0) break;  // starts in the next window
+    // a run starting past the chunk is taken only when all of its bytes are
+    // loaded (its extent depends on its own bytes only); otherwise it starts
+    // the next window
+    const bool past = lp >= kChunk && n > 0;
+    if (past && lp + 2u > lim) break;
     if (lp + kHdrLim > hw.base + 256) hw.load(win, lp, kWin / 4 + 8, lane);
     // the two header bytes from two lanes of the slice, realigned on the
     // scalar unit; SHORT_REPEAT / DIRECT sized inline (branch-free selects),
@@ -638,6 +645,7 @@ __device__ __forceinline__ WalkResult walk(const uint32_t* win, OffT* run_off, u
       rL = uni(rL);
       e = uni(e);
     }
+    if (past && (e != kErrNone || lp + rbytes > lim)) break;  // the next window decides
     if (e != kErrNone || lp + rbytes > lim_all) {
       // the first failing check, in the order parse / segment / window
       if (e == kErrNone)
@@ -1430,6 +1438,20 @@ struct Dense2Lds {
   uint32_t mark[kSlab / 32];
 };
 
+// Union instances (kOptUnion): the run table / successor tables only; the
+// value stages and the marks live past the dense window inside s_win, which a
+// serial window covers whole.
+struct Dense2TabLds {
+  union {
+    struct {
+      uint16_t off[kDenseRuns];
+      uint32_t val[kDenseRuns];
+      uint16_t items[kDenseRuns];
+    } tab;
+    uint16_t nxt[2 * kSlab];
+  };
+};
+
 template <bool kDense>
 __device__ __forceinline__ uint16_t* s_dense_nxt(DenseLds<kDense>& d) {
   if constexpr (kDense) return &d.nxt[0][0];
@@ -1455,13 +1477,19 @@ template <typename T, bool kPositions, int kOpt, int kWinKB, bool kPipe, int kMi
 __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint8_t* __restrict__ p_src, uint64_t p_src_len, int p_is_signed,
     const uint64_t* __restrict__ p_segtab, uint64_t p_nsegs, uint64_t rows_per_group,
-    uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* err,
+    uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* p_err,
     unsigned long long* __restrict__ defer_q, uint32_t defer_par, const RleJob* __restrict__ jobs,
     uint32_t njobs) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
   constexpr uint32_t kChunk = kWin - kMaxRun;
+  // union instances: serial windows of kWinS bytes = the dense window, its
+  // 32-byte slack, the value stages and the marks
+  constexpr bool kUnion = kDense == 2 && (kOpt & kOptUnion) != 0;
+  constexpr uint32_t kWinS = kUnion ? kWin + (uint32_t)(kWaves * kStage * 8 + kSlab / 8) : kWin;
+  constexpr uint32_t kChunkS = kWinS - kMaxRun;
+  static_assert(!kUnion || (kWin + 32) % 8 == 0, "stage alignment");
   static_assert(!kDense || kChunk % kSlab == 0, "dense window chunk must be whole slabs");
   constexpr int kBufs = kPipe ? 2 : 1;
   static_assert(!(kDense && kPipe), "dense mode is a non-pipelined instance");
@@ -1470,7 +1498,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   static_assert(!kDense || 2 * kCap >= kSlab, "DP table must fit the run table");
   static_assert(!kDense || kChunk >= kSlab, "window too small for a slab");
   using OffT = typename std::conditional<kDense == 2, uint16_t, uint32_t>::type;
-  __shared__ __attribute__((aligned(16))) uint32_t s_win[kBufs][kWin / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
+  __shared__ __attribute__((aligned(16))) uint32_t s_win[kBufs][kWinS / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
   __shared__ uint32_t s_ctl[kBufs][16];
   __shared__ uint32_t s_sync[2][2];  // serial passes: {published runs, claimed runs}, by pass parity
   __shared__ DenseLds<kDense == 1> s_dense;
@@ -1481,7 +1509,15 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   uint32_t* s_mark2 = nullptr;
   uint64_t* s_stage2 = nullptr;
   uint16_t* s_items = nullptr;  // serial passes (non-pipelined): work item ends
-  if constexpr (kDense == 2) {
+  if constexpr (kUnion) {
+    __shared__ __attribute__((aligned(16))) Dense2TabLds s_d2;
+    s_items = s_d2.tab.items;
+    s_off[0] = s_d2.tab.off;
+    s_val[0] = s_d2.tab.val;
+    s_nxt2 = s_d2.nxt;
+    s_stage2 = (uint64_t*)((char*)s_win[0] + kWin + 32);
+    s_mark2 = (uint32_t*)((char*)s_win[0] + kWin + 32 + kWaves * kStage * 8);
+  } else if constexpr (kDense == 2) {
     __shared__ __attribute__((aligned(16))) Dense2Lds s_d2;
     s_items = s_d2.tab.items;
     s_off[0] = s_d2.tab.off;
@@ -1518,6 +1554,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   uint64_t value_begin = p_value_begin;
   uint64_t value_end = p_value_begin + p_nvalues;
   T* dst = p_dst;
+  unsigned long long* err = p_err;
   auto bind = [&](const uint64_t gg) -> uint64_t {
     if constexpr (!kMulti) return gg;
     uint32_t lo = 0, hi = njobs - 1;
@@ -1537,6 +1574,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     value_begin = 0;
     value_end = uni64(J->nvalues);
     dst = (T*)uni64((uint64_t)(uintptr_t)J->dst);
+    const uint64_t je = uni64((uint64_t)(uintptr_t)J->err);
+    err = je ? (unsigned long long*)(uintptr_t)je : p_err;
     return gg - uni64(J->seg_base);
   };
 
@@ -1599,7 +1638,11 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     while (pos < seg_end && vi < value_end) {
       const uint32_t wrel = (uint32_t)(pos - bias) & ~15u;
       const uint64_t wpos = bias + wrel;
-      uint32_t need = kWin, keep = 0;
+      // union instances: a window whose runs are known to be long (the probe
+      // is done and the mode is serial) is a serial window of kWinS bytes:
+      // serial passes only, short-run groups expanded without the stage
+      const bool big = kUnion && !dense && !probe;
+      uint32_t need = big ? kWinS : kWin, keep = 0;
       if constexpr ((kOpt & kOptReuse) != 0) {
         // never load past the segment: its runs end at seg_end
         const uint64_t end_rel = (seg_end - bias + 15) & ~15ull;
@@ -1621,7 +1664,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           // every lane issues all of its 16-byte loads before the first LDS
           // write (measured: +4 % over LDS-DMA on a pure window copy)
           typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-          constexpr int kPer = (kWin + kThreads * 16 - 1) / (kThreads * 16);
+          constexpr int kPer = (kWinS + kThreads * 16 - 1) / (kThreads * 16);
           u4 v[kPer];
 #pragma unroll
           for (int i = 0; i < kPer; ++i) {
@@ -1727,10 +1770,13 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             const uint32_t probe_n = (probe && (kDense == 2 || kDefer == 1)) ? (kDense == 2 ? 4u : 8u) : 0u;
             constexpr bool kProbeValues = kDefer == 1 && (kOpt & kOptD3) != 0;
             const uint32_t cap = (kDense == 1 && probe) ? 32u : kCap;
-            const WalkResult w = walk<kWin, kCap, (kOpt & kOptT4) != 0, OffT>(s_win[0], s_off[0], s_val[0], wpos, pos, vi,
-                                                                    seg_end, src_len, value_end, is_signed, err,
-                                                                    lane, need, cap, s_pub, s_items, probe_n,
-                                                                    kProbeValues);
+            const WalkResult w =
+                big ? walk<kWinS, kCap, (kOpt & kOptT4) != 0, OffT>(s_win[0], s_off[0], s_val[0], wpos, pos, vi, seg_end,
+                                                                    src_len, value_end, is_signed, err, lane, need, cap,
+                                                                    s_pub, s_items, probe_n, kProbeValues)
+                    : walk<kWin, kCap, (kOpt & kOptT4) != 0, OffT>(s_win[0], s_off[0], s_val[0], wpos, pos, vi, seg_end,
+                                                                   src_len, value_end, is_signed, err, lane, need, cap,
+                                                                   s_pub, s_items, probe_n, kProbeValues);
             if (lane == 0) {
               s_ctl[0][0] = w.n;
               s_ctl[0][1] = w.stop;
@@ -1765,10 +1811,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
                                          is_signed).L);
               }
 #endif
-              expand_run<kOpt>(s_win[0], kWin / 4 + 8, uni(s_off[0][r0]), vi + uni(s_val[0][r0]), is_signed,
+              expand_run<kOpt>(s_win[0], kWinS / 4 + 8, uni(s_off[0][r0]), vi + uni(s_val[0][r0]), is_signed,
                                value_begin, value_end, dst, lane);
             }
-            else if constexpr (kDense == 2 && (kOpt & kOptD3) != 0)
+            else if (kDense == 2 && (kOpt & kOptD3) != 0 && !big)
               // coalesced stores through the wave's value stage
               dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], s_stage2 + wave * kStage, r0, e, vi,
                                  is_signed, value_begin, value_end, dst, lane);
@@ -1813,6 +1859,13 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               defer_q[3 * gg + 2] = vi;
               __hip_atomic_store(&defer_q[3 * gg], (unsigned long long)defer_par, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
+              // the launch-wide "something was queued" word (after the
+              // launch's last segment entry): written once per launch pair
+              // in the common case (a load first, so a stream whose every
+              // segment queues does not serialise on one address)
+              unsigned long long* any = &defer_q[3 * p_nsegs];
+              if (__hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned long long)defer_par)
+                __hip_atomic_store(any, (unsigned long long)defer_par, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             return;
           }
@@ -1826,7 +1879,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           }
         }
         if (n == 0 && dpos == 0) break;  // nothing consumed (cannot happen for a good window)
-      } while (pos < wpos + kChunk && pos < seg_end && vi < value_end);
+        // a union instance leaves a serial window as soon as its runs turn
+        // short: the next window is a dense one
+        if (big && dense) break;
+      } while (pos < wpos + (big ? kChunkS : kChunk) && pos < seg_end && vi < value_end);
       pwpos = wpos;
       pneed = need;
     }
@@ -1887,6 +1943,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     // wave: an empty share costs one load round) and decodes the rest of
     // each (no counters)
     __shared__ unsigned long long s_flags[kWaves];
+    // nothing queued by the serial launch (long-run streams): one load, exit
+    if (uni64(__hip_atomic_load(&defer_q[3 * p_nsegs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
+        (unsigned long long)defer_par)
+      return;
     const uint64_t per = (p_nsegs + gridDim.x - 1) / gridDim.x;
     const uint64_t g0 = (uint64_t)blockIdx.x * per;
     const uint64_t g1 = min(g0 + per, p_nsegs);
@@ -1927,8 +1987,9 @@ bool rlev2_variant_valid(int v) {
 
 static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
   // {stamp, byte offset, value index} per launch-wide segment, stamps zeroed
-  // at allocation (launch sequence numbers start at 1)
-  if (ctx->defer_cap < nsegs) {
+  // at allocation (launch sequence numbers start at 1); word 3 * nsegs is
+  // the launch's "something was queued" stamp
+  if (ctx->defer_cap < nsegs + 1) {
     if (ctx->d_defer) {
       (void)hipStreamSynchronize(ctx->stream);
       (void)hipFree(ctx->d_defer);
@@ -1945,17 +2006,22 @@ static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
   return ORCG_OK;
 }
 
-// The default's instance for a stream: by density. Wide values (>= 5 stream
-// bytes per value, e.g. W >= 40) stream best through 33 KB windows (4 WG/CU)
-// filled through registers; narrower ones through 21 KB windows (6 WG/CU);
-// both walk run headers with one wave and queue any segment whose first runs
-// are short for the dense instance. Below 1.25 B/value the stream is likely
-// made of short runs (low-cardinality columns: SHORT_REPEAT runs are 0.2-1
-// B/value): the dense instance runs it directly (parallel run discovery,
-// 8.5 KB windows, 6 WG/CU) and falls back to the serial walk inside a segment
-// whose runs are long. Measured: scripts/ab_rlev2.py, profiles/r02/sweep.md.
+// The default's instance for a stream. Wide values (>= 5 stream bytes per
+// value, e.g. W >= 40) stream best through 33 KB windows (4 WG/CU) filled
+// through registers and walked by one wave (writers emit wide random values
+// in long DIRECT runs). Everything else goes to the union instance (6 WG/CU),
+// which routes each window by its own runs: a segment's first window is an
+// 8.5 KB dense window whose inline probe sizes the first runs; short runs in
+// bytes are discovered in parallel (dense passes), long ones are walked, and
+// a segment walking long runs continues in 16.75 KB serial windows (the
+// dense stages and marks are part of them) until its runs turn short again.
+// No whole-stream density guess and no queue: the round-2/3 instances (21 KB
+// serial + queue drain for >= 1.25 B/value, 8.5 KB dense below) lost 7 % on
+// random W=8 and DELTA / PATCHED W=12 and 20 % on short runs of 40-64-bit
+// values to the wrong guess (profiles/r03/sweep.md). Variants 3-5 and 7 pin
+// them for A/B.
 static int default_variant(uint64_t src_len, uint64_t est_values) {
-  return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 4);
+  return src_len >= 5 * est_values ? 2 : 6;
 }
 
 // One launch (or serial + drain pair) of instance `variant` over nsegs
@@ -2043,12 +2109,12 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
   } while (0)
 
   switch (variant) {
-    case 2: ORCG_DEFERRING(kWide | kOptD3, 33, 1, kSer | kOptD3); break;  // 33 KB register-filled serial + dense drain
+    case 2: ORCG_KX(kWide | kOptD3, 33, false, 1, 0, 0, (unsigned)nsegs); break;  // 33 KB register-filled serial, no queue
     case 3: ORCG_DEFERRING(kSer | kOptD3, 21, 6, kSer | kOptD3); break;   // 21 KB serial + dense drain
     case 4: ORCG_KX(kSer | kOptD3, 8, false, 6, 2, 0, (unsigned)nsegs); break;   // dense v3, 8.5 KB
     case 5: ORCG_KX(kSer | kOptD3, 12, false, 5, 2, 0, (unsigned)nsegs); break;  // dense v3, 12.5 KB
-    case 6: ORCG_KX(kSer, 8, false, 6, 2, 0, (unsigned)nsegs); break;            // round-2 dense v2 (A/B)
-    case 7: ORCG_DEFERRING(kWide, 33, 1, kSer); break;                          // round-2 33 KB serial (A/B)
+    case 6: ORCG_KX(kSer | kOptD3 | kOptUnion, 8, false, 6, 2, 0, (unsigned)nsegs); break;  // union: dense 8.5 KB / serial 16.75 KB windows
+    case 7: ORCG_DEFERRING(kWide | kOptD3, 33, 1, kSer | kOptD3); break;  // 33 KB serial + dense drain (round-3 default, A/B)
 #ifdef ORCG_AB_VARIANTS
     case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false); break;  // 21 KB + fast
     case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
@@ -2133,8 +2199,11 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
     for (uint32_t j = 0; j < njobs; ++j) {
       const RleJob& J = jobs[j];
       if (!J.segtab) return set_error(ctx, ORCG_INVALID_ARGUMENT, "row-index job needs a multi-stream instance");
+      unsigned long long* const saved = ctx->d_err;  // the job's own error record
+      if (J.err) ctx->d_err = J.err;
       int rc = launch_rlev2(ctx, J.src, J.src_len, (int)J.is_signed, J.segtab, J.nsegs, false, 0, 0, J.nvalues,
                             J.dst, 8);
+      ctx->d_err = saved;
       if (rc) return rc;
     }
     return ORCG_OK;

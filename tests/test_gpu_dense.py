@@ -12,20 +12,25 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-# default (dense below 1.25 B/value), the serial-walk instances that queue short-run
-# segments (33 KB, 21 KB), the dense instances (8.5 KB, 12.5 KB)
-DENSE_VARIANTS = [0, 2, 3, 4, 5]
+# default (the union instance below 5 B/value), the 33 KB serial instance,
+# the 21 KB serial instance that queues short-run segments, the dense
+# instances (8.5 KB, 12.5 KB), the union instance (8.5 KB dense / 16.75 KB
+# serial windows), the 33 KB serial instance that queues
+DENSE_VARIANTS = [0, 2, 3, 4, 5, 6, 7]
 
 
-def _short_run_stream(rng, signed, n_target, long_every=0):
-    """Run kinds / lengths / values of a stream dominated by short runs."""
+def _short_run_stream(rng, signed, n_target, long_every=0, phase=0):
+    """Run kinds / lengths / values of a stream dominated by short runs
+    (phase > 0: alternately `phase` short runs and `phase // 8` long runs, so
+    a segment's windows switch between dense and serial mode)."""
     vals, kinds, lens = [], [], []
     total = 0
     i = 0
     while total < n_target:
         i += 1
         r = rng.random()
-        if long_every and i % long_every == 0:
+        in_long = phase and (i % (phase + phase // 8)) >= phase
+        if (long_every and i % long_every == 0) or in_long:
             k = int(rng.choice([1, 2, 3]))
             L = int(rng.integers(100, 513))
         elif r < 0.7:
@@ -106,6 +111,40 @@ def test_dense_streams_vs_oracle(signed, long_every):
                 raise AssertionError("variant %d stride %d: %d mismatches, first at %d; got %s want %s" % (
                     variant, stride, bad.size, i, got[max(0, i - 4):i + 12].tolist(),
                     v[max(0, i - 4):i + 12].tolist()))
+    ctx.set_rlev2_variant(0)
+
+
+@pytest.mark.parametrize("phase", [300, 2000])
+def test_window_mode_switches_vs_oracle(phase):
+    """Stretches of short runs and of long runs inside one segment: the
+    union instance (variant 6, the default's below 5 B/value) moves between
+    8.5 KB dense windows and 16.75 KB serial windows; whole streams and value
+    windows against the oracle."""
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(phase)
+    v, kinds, lens = _short_run_stream(rng, True, 600_000, 0, phase)
+    ctx = orc_amd.default_context(0)
+    n = v.size
+    for stride in (50_000, 10_000, 1 << 30):
+        data, pos = _encode_with_positions(orc_amd, v, True, kinds, lens, stride)
+        if stride == 10_000:
+            np.testing.assert_array_equal(oracle.rlev2_decode(data.tobytes(), n, True), v)
+        d_src = torch.from_numpy(data).cuda()
+        d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+        for variant in DENSE_VARIANTS:
+            ctx.set_rlev2_variant(variant)
+            for a, b in [(0, n), (7, n - 11), (123_457, 400_001)]:
+                o = torch.full((b - a,), -7, dtype=torch.int64, device="cuda")
+                orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, b - a, True, o, value_begin=a)
+                ctx.synchronize()
+                got = o.cpu().numpy()
+                if not np.array_equal(got, v[a:b]):
+                    i = int(np.argmax(got != v[a:b]))
+                    raise AssertionError("variant %d stride %d range %d-%d: first mismatch at %d" % (
+                        variant, stride, a, b, a + i))
     ctx.set_rlev2_variant(0)
 
 

@@ -4,6 +4,8 @@ path — host tail parse + decompression, GPU RLEv1/RLEv2/byte/boolean RLE,
 null scatter, dictionary gather, list/map offsets — and compared row by row
 with pyarrow's ORC reader (the reference C++ library) and, where the
 reference ships it, with its expected ColumnPrinter output."""
+import decimal
+
 import numpy as np
 import pytest
 
@@ -180,3 +182,53 @@ def test_crafted_offsets_that_wrap_are_rejected(ctx):
     r = orc_amd.Reader(bad, ctx)
     with pytest.raises(orc_amd.ParseError):
         r.read_stripe(0)
+
+
+def _two_column_file(bad_index_row, bad_scale_row, n=1000):
+    """struct<a:string (DICTIONARY_V2), b:decimal(10,2)>, one stripe, no row
+    index: column a's DATA holds an out-of-range dictionary index at
+    `bad_index_row`, column b's SECONDARY an out-of-range scale (30 for a
+    column of scale 2) at `bad_scale_row` (None: no corruption)."""
+    from orc_craft import field_bytes, field_varint, orc_file, stripe_info, type_msg, varint
+
+    def rle2(vals, signed):
+        v = np.asarray(vals, dtype=np.int64)
+        lens = [min(512, v.size - i) for i in range(0, v.size, 512)]
+        data, _ = orc_amd.encode_runs(v, signed, np.ones(len(lens), np.uint8), np.array(lens, np.uint32))
+        return bytes(data)
+
+    idx = np.zeros(n, np.int64)
+    if bad_index_row is not None:
+        idx[bad_index_row] = 7
+    scales = np.full(n, 2, np.int64)
+    if bad_scale_row is not None:
+        scales[bad_scale_row] = 30
+    a_data, a_len, a_dict = rle2(idx, False), rle2([3, 3, 3], False), b"xyzabcdef"
+    b_data = b"".join(varint(2 * (i % 500)) for i in range(n))  # zigzag varints
+    b_sec = rle2(scales, True)
+    streams = [(1, 1, a_data), (2, 1, a_len), (3, 1, a_dict), (1, 2, b_data), (5, 2, b_sec)]
+    body = b"".join(s[2] for s in streams)
+    sfoot = b"".join(field_bytes(1, field_varint(1, k) + field_varint(2, c) + field_varint(3, len(b)))
+                     for k, c, b in streams)
+    sfoot += field_bytes(2, field_varint(1, 0))                            # root struct: DIRECT
+    sfoot += field_bytes(2, field_varint(1, 3) + field_varint(2, 3))       # a: DICTIONARY_V2, 3 entries
+    sfoot += field_bytes(2, field_varint(1, 2))                            # b: DIRECT_V2
+    types = [type_msg(12, [1, 2], ["a", "b"]), type_msg(7), type_msg(14) + field_varint(5, 10) + field_varint(6, 2)]
+    return orc_file(body + sfoot, [stripe_info(3, 0, len(body), len(sfoot), n)], types, n)
+
+
+def test_first_error_in_column_order(ctx):
+    """Two corrupt columns in one stripe: the error reported is the first
+    column's (the reference decodes a batch column by column, StructColumnReader
+    ::next), although the second column's bad value comes earlier in row
+    order: every column has its own device error record (reader_api.cpp
+    first_error). pyarrow's ORC C++ reader raises the same error on the
+    same file."""
+    ok = orc_amd.Reader(_two_column_file(None, None), ctx).read_stripe(0).to_pylist()
+    assert len(ok) == 1000 and ok[0] == {"a": "xyz", "b": decimal.Decimal("0.00")}
+    with pytest.raises(orc_amd.OrcError, match="Entry index out of range"):
+        orc_amd.Reader(_two_column_file(900, None), ctx).read_stripe(0)
+    with pytest.raises(orc_amd.OrcError, match="Decimal scale out of range"):
+        orc_amd.Reader(_two_column_file(None, 10), ctx).read_stripe(0)
+    with pytest.raises(orc_amd.OrcError, match="Entry index out of range"):
+        orc_amd.Reader(_two_column_file(900, 10), ctx).read_stripe(0)
