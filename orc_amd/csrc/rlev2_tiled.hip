@@ -2006,22 +2006,24 @@ static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
   return ORCG_OK;
 }
 
-// The default's instance for a stream. Wide values (>= 5 stream bytes per
-// value, e.g. W >= 40) stream best through 33 KB windows (4 WG/CU) filled
-// through registers and walked by one wave (writers emit wide random values
-// in long DIRECT runs). Everything else goes to the union instance (6 WG/CU),
-// which routes each window by its own runs: a segment's first window is an
-// 8.5 KB dense window whose inline probe sizes the first runs; short runs in
-// bytes are discovered in parallel (dense passes), long ones are walked, and
-// a segment walking long runs continues in 16.75 KB serial windows (the
-// dense stages and marks are part of them) until its runs turn short again.
-// No whole-stream density guess and no queue: the round-2/3 instances (21 KB
-// serial + queue drain for >= 1.25 B/value, 8.5 KB dense below) lost 7 % on
-// random W=8 and DELTA / PATCHED W=12 and 20 % on short runs of 40-64-bit
-// values to the wrong guess (profiles/r03/sweep.md). Variants 3-5 and 7 pin
-// them for A/B.
+// The default's instance for a stream, by its stream bytes per value
+// (profiles/r03/sweep.md):
+//  * >= 5 B/value (wide values, W >= 40): 33 KB windows (4 WG/CU) filled
+//    through registers, one walking wave, no queue (writers emit wide random
+//    values in long DIRECT runs; the empty queue drain cost 4 us of C2's 290);
+//  * 1.25 - 5 B/value: 21 KB serial windows (6 WG/CU), queueing segments whose
+//    first runs are short by values for the dense drain (long DIRECT / DELTA /
+//    PATCHED_BASE runs of 10-40-bit values: 5.3-6.1 TB/s; short runs of wide
+//    values 20 % slower than the union instance, the price of the rule);
+//  * < 1.25 B/value (low-cardinality columns, SHORT_REPEAT 0.2-1 B/value): the
+//    union instance, which routes each window by its own runs (8.5 KB dense
+//    windows with parallel run discovery, 16.75 KB serial windows once a
+//    segment's runs are long).
+// The dense-capable instances walk long runs 15-20 % slower than the serial
+// ones (at 6 WG/CU they carry 56 B/lane of scratch, the serial ones none), so long-run
+// streams above 1.25 B/value stay on the serial instance.
 static int default_variant(uint64_t src_len, uint64_t est_values) {
-  return src_len >= 5 * est_values ? 2 : 6;
+  return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 6);
 }
 
 // One launch (or serial + drain pair) of instance `variant` over nsegs

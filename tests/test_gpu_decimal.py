@@ -276,7 +276,10 @@ def test_hive11_file_non_throwing_mode_matches_throwing():
     from file_parity import path
 
     r = orc_amd.Reader(path("orc-file-11-format.orc"), orc_amd.default_context(0))
-    want = r.read()
+    # every field but `ts` (a non-UTC writer zone's timestamps, not decoded)
+    fields = [f for f in r.types[0].field_names if f != "ts"]
+    want = r.read(fields)
+    assert all(row["decimal1"] is not None for row in want[:10])
     r.set_hive11_decimal(6, throw_on_overflow=False)
-    got = r.read()
+    got = r.read(fields)
     assert got == want
