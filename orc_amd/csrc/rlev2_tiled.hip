@@ -94,6 +94,8 @@ constexpr int kOptPair = 256;   // full DIRECT runs: two values per lane, one 16
 constexpr int kOptVP = 512;     // serial groups of short runs expanded value-parallel (coalesced stores)
 constexpr int kOptUnion = 1024; // dense v2 instance whose serial (long-run) windows also cover the dense stage and
                                 // marks: one instance routes each window by its runs (dense or serial), no queue
+constexpr int kOptPrefetch = 2048;  // register-filled serial windows: every wave loads its share of the next window
+                                    // into registers as soon as the walk is done, while it expands this one
 
 // Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
 // counts the values of the runs it expands; each pass checks the count
@@ -1623,6 +1625,14 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   if constexpr (!kPipe) {
     uint64_t pwpos = ~0ull;  // previous window (stream offset) and its valid bytes
     uint32_t pneed = 0;
+    // kOptPrefetch: the next window's bytes, loaded into registers during
+    // the previous window's expansion (pf_wrel: its descriptor offset)
+    constexpr bool kPf = (kOpt & kOptPrefetch) != 0 && (kOpt & kOptRegFill) != 0 && (kOpt & kOptReuse) != 0 &&
+                         kDense == 0;
+    typedef uint32_t pf_u4 __attribute__((ext_vector_type(4)));
+    constexpr int kPfPer = kPf ? (int)((kWinS + kThreads * 16 - 1) / (kThreads * 16)) : 1;
+    pf_u4 pf[kPfPer];
+    uint32_t pf_wrel = ~0u, pf_need = 0;
     // wave-uniform mode of the next pass (dense instances only): the
     // segment's first pass is a short serial probe (32 runs in v1, 4 in v2)
     // whose bytes per run pick the mode
@@ -1651,7 +1661,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         // move it to the front instead of re-reading it (source and
         // destination must not overlap: the shift is at least the length;
         // otherwise reload)
-        if (pwpos != ~0ull && pwpos + pneed > wpos && wpos - pwpos >= pwpos + pneed - wpos) {
+        const bool prefetched = kPf && pf_wrel == wrel && pf_need == need;
+        if (!prefetched && pwpos != ~0ull && pwpos + pneed > wpos && wpos - pwpos >= pwpos + pneed - wpos) {
           keep = (uint32_t)(pwpos + pneed - wpos);
           if (keep > need) keep = need;
           const uint32_t so = (uint32_t)(wpos - pwpos);
@@ -1665,18 +1676,28 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           // write (measured: +4 % over LDS-DMA on a pure window copy)
           typedef uint32_t u4 __attribute__((ext_vector_type(4)));
           constexpr int kPer = (kWinS + kThreads * 16 - 1) / (kThreads * 16);
-          u4 v[kPer];
+          if (kPf && prefetched) {
+            // the whole window arrived in registers during the last expansion
 #pragma unroll
-          for (int i = 0; i < kPer; ++i) {
-            const uint32_t off = keep + (uint32_t)(i * kThreads + tid) * 16u;
-            if (off < need)
-              v[i] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, wrel + off, 0, 2));
-          }
+            for (int i = 0; i < kPfPer; ++i) {
+              const uint32_t off = (uint32_t)(i * kThreads + tid) * 16u;
+              if (off < need) *(u4*)((char*)s_win[0] + off) = __builtin_bit_cast(u4, pf[i]);
+            }
+          } else {
+            u4 v[kPer];
 #pragma unroll
-          for (int i = 0; i < kPer; ++i) {
-            const uint32_t off = keep + (uint32_t)(i * kThreads + tid) * 16u;
-            if (off < need) *(u4*)((char*)s_win[0] + off) = v[i];
+            for (int i = 0; i < kPer; ++i) {
+              const uint32_t off = keep + (uint32_t)(i * kThreads + tid) * 16u;
+              if (off < need)
+                v[i] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(rs, wrel + off, 0, 2));
+            }
+#pragma unroll
+            for (int i = 0; i < kPer; ++i) {
+              const uint32_t off = keep + (uint32_t)(i * kThreads + tid) * 16u;
+              if (off < need) *(u4*)((char*)s_win[0] + off) = v[i];
+            }
           }
+          pf_wrel = ~0u;
         } else {
           for (uint32_t off = keep + wave * 1024u; off < need; off += kWaves * 1024u)
             if (off + lane * 16u < need)
@@ -1787,6 +1808,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
             }
             __builtin_amdgcn_s_setprio(0);
           }
+          bool pf_issued = !kPf;
           for (;;) {
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(s_claim, 1u);
@@ -1799,6 +1821,29 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               if (k < (pub & ~kWalkDone) || (pub & kWalkDone)) break;
               if (spin < 2) __builtin_amdgcn_s_sleep(2);
               else __builtin_amdgcn_s_sleep(24);
+            }
+            if constexpr (kPf) {
+              if (!pf_issued && (pub & kWalkDone)) {
+                // the walk is done: if this pass ends the window, load this
+                // thread's share of the next one while the items expand
+                pf_issued = true;
+                const uint64_t npos = pos + uni(s_ctl[0][2]);
+                const uint64_t nvi = vi + uni(s_ctl[0][3]);
+                const uint32_t chunk = big ? kChunkS : kChunk;
+                if (!uni(s_ctl[0][1]) && npos >= wpos + chunk && npos < seg_end && nvi < value_end) {
+                  const uint32_t nwrel = (uint32_t)(npos - bias) & ~15u;
+                  const uint64_t end_rel = (seg_end - bias + 15) & ~15ull;
+                  const uint32_t nneed = end_rel - nwrel < kWinS ? (uint32_t)(end_rel - nwrel) : kWinS;
+#pragma unroll
+                  for (int i = 0; i < kPfPer; ++i) {
+                    const uint32_t off = (uint32_t)(i * kThreads + tid) * 16u;
+                    if (off < nneed)
+                      pf[i] = __builtin_bit_cast(pf_u4, __builtin_amdgcn_raw_buffer_load_b128(rs, nwrel + off, 0, 2));
+                  }
+                  pf_wrel = nwrel;
+                  pf_need = nneed;
+                }
+              }
             }
             if (k >= (pub & ~kWalkDone)) break;  // the walk is done and every item is claimed
             const uint32_t e = uni(s_items[k]);
@@ -2141,6 +2186,9 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     case 28: ORCG_KT(kWide | kOptPair | kOptVP, 33, false, 1, false); break;           // 25 + value-parallel groups
     case 29: ORCG_KT(kSer | kOptPair | kOptVP, 21, false, 6, false); break;            // 27 + value-parallel groups
     case 30: ORCG_DEFERRING(kSer | kOptD3 | kOptVP, 21, 6, kSer | kOptD3); break;     // 3 + value-parallel groups
+    case 31: ORCG_KT(kWide | kOptD3 | kOptPrefetch, 33, false, 1, false); break;      // 2 + next-window prefetch
+    case 32: ORCG_KT(kWide | kOptPrefetch, 24, false, 4, false); break;               // 24 KB + prefetch, 4 WG/CU
+    case 33: ORCG_KT(kWide | kOptPrefetch, 16, false, 5, false); break;               // 16 KB + prefetch, 5 WG/CU
 #endif
     default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "unknown RLEv2 kernel variant");
   }

@@ -31,4 +31,5 @@ done
 for spec in ${SW_SPECS:-"random:64" "random:13" "random:8" "random:1" "delta:12" "patched:12" "repeat:12" "repeat:40" "repeat:64" "shortdirect:16" "shortdirect:64" "shortmix:32"}; do
   run sw_${spec/:/_} 200 python scripts/ab_rlev2.py --data ${spec%%:*} --bits ${spec##*:} --variants ${SW_VARIANTS:-0,3,6,16} --rounds 3 --refs copy,probe5
 done
+run ab64 300 python scripts/ab_rlev2.py --data random --bits 64 --variants ${AB_VARIANTS:-0,2,31,32,33} --rounds 5 --refs copy,probe5
 echo done >> $OUT/status.log
