@@ -13,10 +13,9 @@
 // thread); wave 0 walks the control bytes on the scalar unit, reading them
 // from a 256-byte slice of the window held one dword per lane (v_readlane, no
 // LDS round trip per group), into a group table {window offset, first decoded
-// byte}; then every thread expands decoded bytes tid, tid + 256, ... of the
-// pass, finding each one's group by a binary search of the table (runs: the
-// value byte; literals: their byte), so stores are coalesced across the
-// workgroup whatever the mix of runs and literals.
+// byte}; then the waves expand the groups, one group per wave at a time and
+// one decoded byte per lane (runs: the value byte; literals: their byte), so
+// every store instruction writes one contiguous span.
 // In boolean mode every decoded byte becomes 8 output rows (chars 0/1).
 #include "rlev2_device.hh"
 
@@ -142,20 +141,20 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
     }
     __syncthreads();
     const uint32_t n = s_ctl[0], np = s_ctl[1], nv = s_ctl[2], stop = s_ctl[3];
-    // every thread expands decoded bytes tid, tid + 256, ... (their groups
-    // only move forward: each search starts at the previous one's group)
-    uint32_t gl = 0;
-    for (uint32_t d = (uint32_t)tid; d < nv; d += kBThreads) {
-      uint32_t hi = n - 1;
-      while (gl < hi) {
-        const uint32_t mid = (gl + hi + 1) >> 1;
-        if (s_start[mid] <= d) gl = mid;
-        else hi = mid - 1;
-      }
-      const uint32_t o = s_off[gl];
+    // group-parallel expansion: wave w takes groups w, w + 4, ...; its lanes
+    // take the group's decoded bytes lane, lane + 64, ... (a group is <= 130
+    // bytes: at most three rounds); the group's table entries are uniform
+    // loads, its literal bytes consecutive ones, and every round stores one
+    // contiguous span (8 rows per lane in boolean mode)
+    for (uint32_t gi = (uint32_t)wave; gi < n; gi += kBThreads / kWave) {
+      const uint32_t o = s_off[gi];
+      const uint32_t d0 = s_start[gi], len = s_start[gi + 1] - d0;
       const uint32_t h = s_bytes[o];
-      const uint32_t b = s_bytes[h < 0x80 ? o + 1u : o + 1u + (d - s_start[gl])];
-      emit<kBool>(dst, vi + d, b, begin, end);
+      const uint32_t rb = s_bytes[o + 1];
+      for (uint32_t j = (uint32_t)lane; j < len; j += kWave) {
+        const uint32_t b = h < 0x80 ? rb : s_bytes[o + 1u + j];
+        emit<kBool>(dst, vi + d0 + j, b, begin, end);
+      }
     }
     __syncthreads();  // the window and the table are rewritten by the next pass
     if (stop) return;

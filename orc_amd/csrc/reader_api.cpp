@@ -1168,7 +1168,18 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
       } else {
         kind = v1 ? 1 : 2;
       }
-      if (sb.pos) continue;  // cut by the row index
+      // cut by the row index, unless its row groups are too coarse to fill
+      // the GPU: a child column's row groups hold several rows per parent
+      // row (a list<int> stream of 10k parent rows: ~40k values, 160 KB),
+      // one workgroup each walks them serially while most of the GPU idles;
+      // such a stream gets a host plan (header walk only) with 16 KB / 1 KB
+      // segments, as streams without a row index do
+      if (sb.pos) {
+        const uint64_t per_group = hs.ngroups ? sb.len / hs.ngroups : 0;
+        if (per_group <= (kind == 0 ? (2u << 10) : (16u << 10))) continue;
+        sb.pos = false;
+        sb.trip.clear();
+      }
       rle.push_back(&sb);
       rle_kind.push_back(kind);
     }
@@ -1246,7 +1257,13 @@ int orcg_reader::first_error(int inline_rc) {
     if (rec[col] != kNoError) {
       const uint32_t code = (uint32_t)(rec[col] & 0xff);
       ctx->last_error_value = rec[col] >> 8;
-      return fail(dev_error_status(code), dev_error_message(code));
+      std::string m = dev_error_message(code);
+      if (m == "unknown device error") {
+        char b[96];
+        snprintf(b, sizeof b, " (column %u, record 0x%llx)", col, (unsigned long long)rec[col]);
+        m += b;
+      }
+      return fail(dev_error_status(code), m);
     }
   }
   if (inline_rc) return fail(inline_rc, inline_msg);
