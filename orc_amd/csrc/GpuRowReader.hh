@@ -204,9 +204,17 @@ class RowReader {
   orcg_row_reader* rr_ = nullptr;
   bool lazy_ = false;
   bool tight_ = false;
-  // the current stripe's dictionaries, shared by its batches (lazy decoding)
+  // the current stripe's dictionaries, shared by its batches (lazy decoding:
+  // StringDictionary; eager: the blob the batches' data pointers point into,
+  // as the reference's batches point into the column reader's dictionary)
   uint64_t dict_stripe_ = ~0ull;
   std::map<uint32_t, std::shared_ptr<StringDictionary>> dicts_;
+  std::map<uint32_t, std::shared_ptr<std::vector<char>>> blobs_;
+  // per type: the children fill() visits (struct: the selected fields)
+  std::vector<std::vector<uint32_t>> subs_;
+  std::vector<uint8_t> subs_known_;
+  const std::vector<uint32_t>& subs(uint32_t id, uint32_t kind);
+  void new_stripe();
 };
 
 class Reader {
@@ -402,6 +410,28 @@ inline void narrow_copy(std::vector<T>& dst, const void* src, uint64_t n, uint64
   for (uint64_t i = 0; i < n; ++i) dst[i] = static_cast<T>(p[i]);
 }
 
+inline const std::vector<uint32_t>& RowReader::subs(uint32_t id, uint32_t kind) {
+  if (id >= subs_.size()) {
+    subs_.resize(id + 1);
+    subs_known_.resize(id + 1, 0);
+  }
+  if (!subs_known_[id]) {
+    for (uint32_t s : r_.getSubtypes(id))
+      if (kind != ORCG_TYPE_STRUCT || isSelected(s)) subs_[id].push_back(s);
+    subs_known_[id] = 1;
+  }
+  return subs_[id];
+}
+
+inline void RowReader::new_stripe() {
+  const uint64_t stripe = orcg_row_reader_stripe(rr_);
+  if (stripe != dict_stripe_) {
+    dicts_.clear();
+    blobs_.clear();
+    dict_stripe_ = stripe;
+  }
+}
+
 inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
   orcg_column_view v;
   uint64_t first = 0, n = 0;
@@ -414,9 +444,7 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
   b.hasNulls = v.has_nulls != 0;
   if (b.hasNulls) Reader::hcopy(b.notNull, v.not_null, n, first);
   else b.notNull.assign(n, 1);
-  std::vector<uint32_t> subs;
-  for (uint32_t s : r_.getSubtypes(id))
-    if (v.kind != ORCG_TYPE_STRUCT || isSelected(s)) subs.push_back(s);
+  const std::vector<uint32_t>& subs = this->subs(id, v.kind);
   if (auto* l = dynamic_cast<LongVectorBatch*>(&b)) {
     Reader::hcopy(l->data, v.data, n, first);
   } else if (auto* i32 = dynamic_cast<IntVectorBatch*>(&b)) {
@@ -434,11 +462,7 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
     // one host dictionary per stripe shared by its batches
     e->isEncoded = true;
     Reader::hcopy(e->index, v.index, n, first);
-    const uint64_t stripe = orcg_row_reader_stripe(rr_);
-    if (stripe != dict_stripe_) {
-      dicts_.clear();
-      dict_stripe_ = stripe;
-    }
+    new_stripe();
     std::shared_ptr<StringDictionary>& dict = dicts_[id];
     if (!dict) {
       dict = std::make_shared<StringDictionary>();
@@ -451,24 +475,32 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
     for (uint64_t i = 0; i < n; ++i)
       if (!b.hasNulls || b.notNull[i]) dict->getValueByIndex(e->index[i], e->data[i], e->length[i]);
   } else if (auto* s = dynamic_cast<StringVectorBatch*>(&b)) {
-    std::vector<int64_t> start;
-    Reader::hcopy(start, v.data, n, first);
+    const int64_t* start = (const int64_t*)v.data + first;  // the slab's (start, length) pairs
     Reader::hcopy(s->length, v.length, n, first);
-    // dictionary: the whole blob; direct: the byte span the batch covers
-    uint64_t lo = 0, hi = v.blob_len;
-    if (!v.index) {
-      lo = ~0ull;
-      hi = 0;
+    s->data.resize(n);
+    if (v.index) {
+      // dictionary: the stripe's blob, copied once and shared by its batches
+      new_stripe();
+      std::shared_ptr<std::vector<char>>& blob = blobs_[id];
+      if (!blob) {
+        blob = std::make_shared<std::vector<char>>();
+        Reader::hcopy(*blob, v.blob, v.blob_len);
+      }
+      s->blob.clear();
+      char* base = blob->data();
+      for (uint64_t i = 0; i < n; ++i) s->data[i] = base + (s->length[i] > 0 ? start[i] : 0);
+    } else {
+      // direct: the byte span the batch covers
+      uint64_t lo = ~0ull, hi = 0;
       for (uint64_t i = 0; i < n; ++i)
         if (s->length[i] > 0) {
           lo = std::min<uint64_t>(lo, (uint64_t)start[i]);
           hi = std::max<uint64_t>(hi, (uint64_t)(start[i] + s->length[i]));
         }
       if (lo == ~0ull) lo = hi = 0;
+      Reader::hcopy(s->blob, v.blob, hi - lo, lo);
+      for (uint64_t i = 0; i < n; ++i) s->data[i] = s->blob.data() + (s->length[i] > 0 ? start[i] - (int64_t)lo : 0);
     }
-    Reader::hcopy(s->blob, v.blob, hi - lo, lo);
-    s->data.resize(n);
-    for (uint64_t i = 0; i < n; ++i) s->data[i] = s->blob.data() + (s->length[i] > 0 ? start[i] - (int64_t)lo : 0);
   } else if (auto* d64 = dynamic_cast<Decimal64VectorBatch*>(&b)) {
     const orcg_type_info t = r_.getType(id);
     d64->precision = (int32_t)t.precision;

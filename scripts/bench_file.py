@@ -122,7 +122,8 @@ def row_reader_leg(path, nrows, stripes_wall):
     src = os.path.join(ROOT, "tests", "cxx", "reader_test.cpp")
     exe = os.path.join(ROOT, "tests", "cxx", "build", "reader_test")
     os.makedirs(os.path.dirname(exe), exist_ok=True)
-    if not os.path.exists(exe) or os.path.getmtime(exe) < os.path.getmtime(src):
+    hdr = os.path.join(ROOT, "orc_amd", "csrc", "GpuRowReader.hh")
+    if not os.path.exists(exe) or os.path.getmtime(exe) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", src, "-o",
                                exe, "-L" + os.path.join(ROOT, "orc_amd"), "-lorcgpu",
                                "-Wl,-rpath," + os.path.join(ROOT, "orc_amd"), "-Wl,-rpath,/opt/rocm/lib"])
