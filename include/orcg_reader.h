@@ -158,6 +158,12 @@ int orcg_reader_column(const orcg_reader* r, uint32_t type_id, orcg_column_view*
  * decodes stripe i. orcg_reader_stripe_column(r, k, ...) views the k-th. */
 int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count);
 int orcg_reader_stripe_column(const orcg_reader* r, uint64_t k, uint32_t type_id, orcg_column_view* out);
+/* Measurement helper (no reference counterpart): prepare stripe `stripe`
+ * once (host decompression, plans), then decode it `iters` times back to
+ * back; *decode_s / *h2d_s = average device-decode / upload seconds per
+ * decode. Separates kernel time from the idle gaps of a host-bound read. */
+int orcg_reader_bench_stripe_decode(orcg_reader* r, uint64_t stripe, uint32_t iters, double* decode_s,
+                                    double* h2d_s);
 
 /* ---- RowReader (c++/include/orc/Reader.hh:640-790; c++/src/Reader.cc
  * RowReaderImpl) over the GPU stripe decode. Batches hold at most `capacity`

@@ -159,6 +159,8 @@ SIGNATURES += [
     ("orcg_reader_read_stripe", [vp, u64], i32),
     ("orcg_reader_column", [vp, u32, ctypes.POINTER(ColumnView)], i32),
     ("orcg_reader_read_stripes", [vp, u64, u64], i32),
+    ("orcg_reader_bench_stripe_decode", [vp, u64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_double),
+                                         ctypes.POINTER(ctypes.c_double)], i32),
     ("orcg_reader_stripe_column", [vp, u64, u32, ctypes.POINTER(ColumnView)], i32),
     ("orcg_reader_copy_to_host", [vp, vp, vp, u64], i32),
     ("orcg_reader_last_timings", [vp, ctypes.POINTER(ctypes.c_double)], i32),

@@ -411,10 +411,14 @@ inline void narrow_copy(std::vector<T>& dst, const void* src, uint64_t n, uint64
 }
 
 inline const std::vector<uint32_t>& RowReader::subs(uint32_t id, uint32_t kind) {
-  if (id >= subs_.size()) {
-    subs_.resize(id + 1);
-    subs_known_.resize(id + 1, 0);
+  if (subs_.empty()) {
+    // sized once for every type: fill() holds a reference across its
+    // recursive calls, so the outer vector never reallocates
+    const uint32_t nt = orcg_reader_num_types(r_.get());
+    subs_.resize(nt);
+    subs_known_.assign(nt, 0);
   }
+  if (id >= subs_.size()) throw InvalidArgument("type id " + std::to_string(id) + " out of range");
   if (!subs_known_[id]) {
     for (uint32_t s : r_.getSubtypes(id))
       if (kind != ORCG_TYPE_STRUCT || isSelected(s)) subs_[id].push_back(s);

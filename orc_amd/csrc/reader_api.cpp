@@ -1878,6 +1878,26 @@ int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe) {
   return r->read_stripes(stripe, 1);
 }
 
+int orcg_reader_bench_stripe_decode(orcg_reader* r, uint64_t stripe, uint32_t iters, double* decode_s, double* h2d_s) {
+  if (!r || !decode_s || !h2d_s || iters == 0) return ORCG_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(r->mu);
+  if (!r->ctx) return r->fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
+  if (stripe >= r->footer.stripes.size()) return r->fail(ORCG_INVALID_ARGUMENT, "stripe index out of range");
+  hipSetDevice(r->ctx->device);
+  int rc = r->prepare(stripe, r->stages[0]);
+  if (rc) return rc;
+  if (r->slots.empty()) r->slots.emplace_back(new DevSlot());
+  // one untimed decode (allocations), then `iters` back-to-back decodes of
+  // the prepared stripe: the GPU never waits for host decompression
+  rc = r->upload_and_decode(r->stages[0], *r->slots[0]);
+  for (auto& t : r->timings) t = 0;
+  for (uint32_t i = 0; i < iters && !rc; ++i) rc = r->upload_and_decode(r->stages[0], *r->slots[0]);
+  r->nslots = rc ? 0 : 1;
+  *decode_s = r->timings[4] / iters;
+  *h2d_s = r->timings[3] / iters;
+  return rc;
+}
+
 int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count) {
   if (!r) return ORCG_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(r->mu);

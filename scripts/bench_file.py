@@ -151,6 +151,9 @@ def main():
     ap.add_argument("--row-reader", action="store_true",
                     help="also time the C++ RowReader scan loop (tests/cxx/reader_test --bench, batch 1024)")
     ap.add_argument("--cpu-threads", default="1,16", help="pyarrow ORC reader thread counts for the CPU legs")
+    ap.add_argument("--steady", type=int, default=10,
+                    help="also decode each prepared stripe this many times back to back (GPU never waiting for the "
+                         "host): device decode at steady clocks; 0 = skip")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; gloo lets "
                                                       "ranks share one GPU)")
     args = ap.parse_args()
@@ -214,6 +217,23 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
     stats = r.last_stream_stats()
+
+    # steady state: each stripe prepared once and decoded back to back, so
+    # the kernels run at the clocks of a busy GPU (the pipelined read leaves
+    # the GPU idle while the host decompresses, and its kernels then run at
+    # idle clocks)
+    steady = None
+    if args.steady and last > first:
+        import ctypes
+        dec, h2d = ctypes.c_double(), ctypes.c_double()
+        tot_dec = tot_h2d = 0.0
+        for s in range(first, last):
+            orc_amd._lib.check(r._L.orcg_reader_bench_stripe_decode(r._h, s, args.steady, ctypes.byref(dec),
+                                                                    ctypes.byref(h2d)), r._err)
+            tot_dec += dec.value
+            tot_h2d += h2d.value
+        steady = {"device_decode_s": round(tot_dec, 5), "h2d_s": round(tot_h2d, 5), "iters_per_stripe": args.steady}
+        r.read_stripes_device(first, last - first)  # the views below describe the full read again
 
     # decoded bytes (device batch layout) of this rank's stripes
     dec_bytes = 0
@@ -295,6 +315,10 @@ def main():
             "device_roofline_s": round((stats["stage_bytes"] + dec_bytes) / 6e12, 5),
             "device_vs_roofline": round(ph[4] / max((stats["stage_bytes"] + dec_bytes) / 6e12, 1e-12), 1),
             "rle_streams": stats,
+            "device_decode_steady": None if steady is None else dict(
+                steady, Mrows_per_s=round(my_rows / max(steady["device_decode_s"], 1e-9) / 1e6, 1),
+                vs_roofline=round(steady["device_decode_s"] / max((stats["stage_bytes"] + dec_bytes) / 6e12, 1e-12),
+                                  1)),
             "host_batch_copy_s": None if host is None else round(host, 3),
             "concat": concat,
             "row_reader": rowreader,
