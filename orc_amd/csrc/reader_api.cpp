@@ -1168,15 +1168,18 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
       } else {
         kind = v1 ? 1 : 2;
       }
-      // cut by the row index, unless its row groups are too coarse to fill
-      // the GPU: a child column's row groups hold several rows per parent
-      // row (a list<int> stream of 10k parent rows: ~40k values, 160 KB),
-      // one workgroup each walks them serially while most of the GPU idles;
-      // such a stream gets a host plan (header walk only) with 16 KB / 1 KB
-      // segments, as streams without a row index do
+      // cut by the row index, unless a byte-RLE stream's row groups are too
+      // coarse to fill the GPU: a child column's row groups hold several
+      // rows per parent row (C5's list items: ~40k PRESENT bits, 5 KB per
+      // row group), one workgroup each while most of the GPU idles; such a
+      // stream gets a host plan with 1 KB segments, as streams without a row
+      // index do (its walk hops ~129 bytes at a time, in address order: cheap
+      // on the host). Integer streams keep the row index: their host walk
+      // chases run headers ~2 KB apart through memory (~45 ns a run, 0.9 ms
+      // for a 42 MB stream), which lands on the host-bound critical path
       if (sb.pos) {
         const uint64_t per_group = hs.ngroups ? sb.len / hs.ngroups : 0;
-        if (per_group <= (kind == 0 ? (2u << 10) : (16u << 10))) continue;
+        if (kind != 0 || per_group <= (2u << 10)) continue;
         sb.pos = false;
         sb.trip.clear();
       }

@@ -94,6 +94,8 @@ constexpr int kOptPair = 256;   // full DIRECT runs: two values per lane, one 16
 constexpr int kOptVP = 512;     // serial groups of short runs expanded value-parallel (coalesced stores)
 constexpr int kOptUnion = 1024; // dense v2 instance whose serial (long-run) windows also cover the dense stage and
                                 // marks: one instance routes each window by its runs (dense or serial), no queue
+constexpr int kOptScan = 4096;      // dense discovery: block entries by a wave scan of entry-state functions (DPP,
+                                    // no LDS gathers), the pointer-doubling chain only when a run jumps too far
 constexpr int kOptPrefetch = 2048;  // register-filled serial windows: every wave loads its share of the next window
                                     // into registers as soon as the walk is done, while it expands this one
 
@@ -1153,64 +1155,150 @@ __device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT
     }
   }
   PROF_MARK(3);
-  // (2) the chain from slab position 0 by pointer doubling over two
-  // successor tables (read one, write the other: one barrier per level)
-  uint32_t na[kBlk];
+  // (2) every block's entry on the chain from slab position 0
+  bool has = false;
+  uint32_t eb = 0;
+  bool chained = false;
+  if constexpr ((kOpt & kOptScan) != 0) {
+    // f_t: entry state -> entry state of block t + 1, over 16 states (0-7:
+    // offset in block t; 8-15: offset in block t + 1, block t skipped), one
+    // byte each (0x80 = dead: unknown run, or past the pass's limit); a wave
+    // inclusive scan of the compositions (DPP, no LDS) gives each block's
+    // entry; a run from an entry that jumps past the next two blocks cannot
+    // be expressed, and sends the slab to the pointer-doubling chain below
+    // when (and only when) the chain itself takes it
+    uint32_t fd[4];
+    uint32_t ovf = 0;
 #pragma unroll
-  for (int e = 0; e < (int)kBlk; ++e) {
-    const uint32_t x = ent[e] & 0x7fffu;
-    na[e] = ((ent[e] & kDpUnknown) || x >= lim) ? (uint32_t)kSink : x;
+    for (int x = 0; x < 16; ++x) {
+      uint32_t y;
+      if (x < (int)kBlk) {
+        const uint32_t en = ent[x];
+        const uint32_t q = en & 0x7fffu;
+        const bool dead = (en & kDpUnknown) || q >= lim;
+        const uint32_t rel = q - (lo + kBlk);
+        const bool far = !dead && rel >= 16u;
+        ovf |= far ? (1u << x) : 0u;
+        y = (dead || far) ? 0x80u : rel;
+      } else {
+        y = (uint32_t)x - kBlk;
+      }
+      if ((x & 3) == 0) fd[x >> 2] = y;
+      else fd[x >> 2] |= y << (8 * (x & 3));
+    }
+    auto fget = [](const uint32_t* d, uint32_t y) -> uint32_t {
+      const uint32_t w = y < 8u ? (y < 4u ? d[0] : d[1]) : (y < 12u ? d[2] : d[3]);
+      return (w >> ((y & 3u) * 8u)) & 0xffu;
+    };
+    // own <- own o fetched (fetched applied first); lanes without a source
+    // keep the identity (bound_ctrl off: the old operand)
+    auto step = [&](auto ctrl_tag, auto mask_tag) {
+      constexpr int kCtrl = decltype(ctrl_tag)::value, kMask = decltype(mask_tag)::value;
+      const uint32_t idn[4] = {0x03020100u, 0x07060504u, 0x0B0A0908u, 0x0F0E0D0Cu};
+      uint32_t f[4], r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        f[k] = (uint32_t)__builtin_amdgcn_update_dpp((int)idn[k], (int)fd[k], kCtrl, kMask, 0xf, false);
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const uint32_t y = (f[x >> 2] >> (8 * (x & 3))) & 0xffu;
+        const uint32_t z = y < 16u ? fget(fd, y) : 0x80u;
+        if ((x & 3) == 0) r[x >> 2] = z;
+        else r[x >> 2] |= z << (8 * (x & 3));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) fd[k] = r[k];
+    };
+    step(std::integral_constant<int, 0x111>{}, std::integral_constant<int, 0xf>{});  // row_shr:1
+    step(std::integral_constant<int, 0x112>{}, std::integral_constant<int, 0xf>{});  // row_shr:2
+    step(std::integral_constant<int, 0x114>{}, std::integral_constant<int, 0xf>{});  // row_shr:4
+    step(std::integral_constant<int, 0x118>{}, std::integral_constant<int, 0xf>{});  // row_shr:8
+    step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xa>{});  // row_bcast:15
+    step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xc>{});  // row_bcast:31
+    // the wave totals through LDS (the marks' words are free here)
+    if (lane == kWave - 1) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s_mark[4 * wave + k] = fd[k];
+    }
+    if (tid == 0) s_mark[16] = 0;
+    __syncthreads();
+    uint32_t xw = 0;  // the wave's entry state: the slab starts at position 0
+    for (int w = 0; w < wave; ++w) {
+      const uint32_t t[4] = {s_mark[4 * w], s_mark[4 * w + 1], s_mark[4 * w + 2], s_mark[4 * w + 3]};
+      xw = xw < 16u ? fget(t, xw) : 0x80u;
+    }
+    const uint32_t nxt = xw < 16u ? fget(fd, xw) : 0x80u;  // block t + 1's entry state
+    const uint32_t cur = (uint32_t)__builtin_amdgcn_update_dpp((int)xw, (int)nxt, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    has = cur < kBlk;
+    eb = has ? cur : 0u;
+    const bool bad = has && ((ovf >> eb) & 1u);
+    if (__ballot(bad) != 0 && lane == 0) s_mark[16] = 1u;
+    __syncthreads();
+    chained = s_mark[16] != 0;
+    if (chained) __syncthreads();  // every wave has read the flag before the chain rewrites the marks
+  } else {
+    chained = true;
   }
-  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  auto put8 = [&](uint16_t* t) {
-    u4 w;
-    w.x = na[0] | na[1] << 16;
-    w.y = na[2] | na[3] << 16;
-    w.z = na[4] | na[5] << 16;
-    w.w = na[6] | na[7] << 16;
-    *(u4*)(t + lo) = w;
-  };
-  uint16_t* ta = s_nxt;
-  uint16_t* tb = s_nxt + kSlab;
-  put8(ta);
-  if (tid < (int)(kSlab / 32)) s_mark[tid] = tid == 0;  // position 0 starts the chain
-  __syncthreads();
-#pragma unroll 1
-  for (int lev = 0; lev < 8; ++lev) {
-    const uint32_t m8 = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
-    if (m8) {
-      // marked positions mark their successor (marks only grow, and every
-      // marked position is a chain element, so racing with this level's
-      // readers is harmless)
-#pragma unroll
-      for (int e = 0; e < (int)kBlk; ++e) {
-        const bool go = ((m8 >> e) & 1u) && na[e] != kSink;
-        if constexpr ((kOpt & kOptD3) != 0) {
-          if (go) atomicOr(&s_mark[na[e] >> 5], 1u << (na[e] & 31u));
-        } else {
-          const uint32_t n = go ? na[e] : 0u;
-          atomicOr(&s_mark[n >> 5], go ? 1u << (n & 31u) : 0u);
+  if (chained) {
+    // (2) the chain from slab position 0 by pointer doubling over two
+    // successor tables (read one, write the other: one barrier per level)
+    uint32_t na[kBlk];
+  #pragma unroll
+    for (int e = 0; e < (int)kBlk; ++e) {
+      const uint32_t x = ent[e] & 0x7fffu;
+      na[e] = ((ent[e] & kDpUnknown) || x >= lim) ? (uint32_t)kSink : x;
+    }
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    auto put8 = [&](uint16_t* t) {
+      u4 w;
+      w.x = na[0] | na[1] << 16;
+      w.y = na[2] | na[3] << 16;
+      w.z = na[4] | na[5] << 16;
+      w.w = na[6] | na[7] << 16;
+      *(u4*)(t + lo) = w;
+    };
+    uint16_t* ta = s_nxt;
+    uint16_t* tb = s_nxt + kSlab;
+    put8(ta);
+    if (tid < (int)(kSlab / 32)) s_mark[tid] = tid == 0;  // position 0 starts the chain
+    __syncthreads();
+  #pragma unroll 1
+    for (int lev = 0; lev < 8; ++lev) {
+      const uint32_t m8 = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
+      if (m8) {
+        // marked positions mark their successor (marks only grow, and every
+        // marked position is a chain element, so racing with this level's
+        // readers is harmless)
+  #pragma unroll
+        for (int e = 0; e < (int)kBlk; ++e) {
+          const bool go = ((m8 >> e) & 1u) && na[e] != kSink;
+          if constexpr ((kOpt & kOptD3) != 0) {
+            if (go) atomicOr(&s_mark[na[e] >> 5], 1u << (na[e] & 31u));
+          } else {
+            const uint32_t n = go ? na[e] : 0u;
+            atomicOr(&s_mark[n >> 5], go ? 1u << (n & 31u) : 0u);
+          }
         }
       }
+  #pragma unroll
+      for (int e = 0; e < (int)kBlk; ++e) {
+        const bool valid = na[e] != kSink;
+        const uint32_t v = ta[valid ? na[e] : lo + (uint32_t)e];
+        na[e] = valid ? v : (uint32_t)kSink;
+      }
+      put8(tb);
+      uint16_t* t = ta;
+      ta = tb;
+      tb = t;
+      __syncthreads();
     }
-#pragma unroll
-    for (int e = 0; e < (int)kBlk; ++e) {
-      const bool valid = na[e] != kSink;
-      const uint32_t v = ta[valid ? na[e] : lo + (uint32_t)e];
-      na[e] = valid ? v : (uint32_t)kSink;
-    }
-    put8(tb);
-    uint16_t* t = ta;
-    ta = tb;
-    tb = t;
-    __syncthreads();
+    const uint32_t mb = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
+    has = mb != 0;
+    eb = has ? (uint32_t)__builtin_ctz(mb) : 0u;
   }
   PROF_MARK(4);
   // (3) the block's entry, its runs (a forward pass over the DP registers),
   // one combined scan of the values and run counts
-  const uint32_t mb = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
-  const bool has = mb != 0;
-  const uint32_t eb = has ? (uint32_t)__builtin_ctz(mb) : 0u;
   uint32_t ee = ent[0];
 #pragma unroll
   for (int k = 1; k < (int)kBlk; ++k) ee = eb == (uint32_t)k ? ent[k] : ee;
@@ -2189,6 +2277,8 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     case 31: ORCG_KT(kWide | kOptD3 | kOptPrefetch, 33, false, 1, false); break;      // 2 + next-window prefetch
     case 32: ORCG_KT(kWide | kOptPrefetch, 24, false, 4, false); break;               // 24 KB + prefetch, 4 WG/CU
     case 33: ORCG_KT(kWide | kOptPrefetch, 16, false, 5, false); break;               // 16 KB + prefetch, 5 WG/CU
+    case 34: ORCG_KT(kSer | kOptD3 | kOptUnion | kOptScan, 8, false, 6, 2); break;      // union + scan chain
+    case 35: ORCG_KT(kSer | kOptD3 | kOptScan, 8, false, 6, 2); break;                  // dense v3 (4) + scan chain
 #endif
     default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "unknown RLEv2 kernel variant");
   }

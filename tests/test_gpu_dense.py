@@ -5,6 +5,8 @@ runs (SHORT_REPEAT-heavy low-cardinality columns, short DIRECT / DELTA runs)
 with long and PATCHED_BASE runs mixed in, so a window switches between the
 serial walk and dense mode. Bit-exact against the CPU oracle.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -12,11 +14,14 @@ from oracle import oracle
 
 pytestmark = pytest.mark.gpu
 
-# default (the union instance below 5 B/value), the 33 KB serial instance,
+# default (three density tiers: 33 KB serial, 21 KB serial + queue, union), the 33 KB serial instance,
 # the 21 KB serial instance that queues short-run segments, the dense
 # instances (8.5 KB, 12.5 KB), the union instance (8.5 KB dense / 16.75 KB
 # serial windows), the 33 KB serial instance that queues
 DENSE_VARIANTS = [0, 2, 3, 4, 5, 6, 7]
+# A/B instances of the tuning build (ORCG_LIB=liborcgpu_ab.so), e.g.
+# ORCG_TEST_EXTRA_VARIANTS=34,35
+DENSE_VARIANTS += [int(v) for v in os.environ.get("ORCG_TEST_EXTRA_VARIANTS", "").split(",") if v]
 
 
 def _short_run_stream(rng, signed, n_target, long_every=0, phase=0):
