@@ -2113,7 +2113,9 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
 bool rlev2_variant_valid(int v) {
   if (v >= 0 && v <= 7) return true;
 #ifdef ORCG_AB_VARIANTS
-  if (v >= 8 && v <= kMaxRlev2Variant) return true;
+  // 28-30 (value-parallel short-run groups) were dropped: wrong on short
+  // runs of wide values (tests/test_gpu_dense.py test_wide_short_runs_vs_oracle)
+  if (v >= 8 && v <= kMaxRlev2Variant && (v < 28 || v > 30)) return true;
 #endif
   return false;
 }
@@ -2271,9 +2273,6 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     case 25: ORCG_KT(kWide | kOptPair, 33, false, 1, false); break;                    // 20 + 16-byte pair stores
     case 26: ORCG_DEFERRING(kWide | kOptD3 | kOptPair, 33, 1, kSer | kOptD3 | kOptPair); break;  // 2 + pair stores
     case 27: ORCG_KT(kSer | kOptPair, 21, false, 6, false); break;                     // 16 + pair stores
-    case 28: ORCG_KT(kWide | kOptPair | kOptVP, 33, false, 1, false); break;           // 25 + value-parallel groups
-    case 29: ORCG_KT(kSer | kOptPair | kOptVP, 21, false, 6, false); break;            // 27 + value-parallel groups
-    case 30: ORCG_DEFERRING(kSer | kOptD3 | kOptVP, 21, 6, kSer | kOptD3); break;     // 3 + value-parallel groups
     case 31: ORCG_KT(kWide | kOptD3 | kOptPrefetch, 33, false, 1, false); break;      // 2 + next-window prefetch
     case 32: ORCG_KT(kWide | kOptPrefetch, 24, false, 4, false); break;               // 24 KB + prefetch, 4 WG/CU
     case 33: ORCG_KT(kWide | kOptPrefetch, 16, false, 5, false); break;               // 16 KB + prefetch, 5 WG/CU
