@@ -42,8 +42,19 @@ def _decodable(reader, batch):
     return [n for n, s in zip(root.field_names, root.subtypes) if ok(s)]
 
 
+def _has_timestamp(reader, tid):
+    t = reader.types[tid]
+    return t.kind in (9, 18) or any(_has_timestamp(reader, s) for s in t.subtypes)
+
+
 def _check_rows(reader, batch, want_rows, first, where):
     fields = _decodable(reader, batch)
+    if fields is not None:
+        # the only fields left out are those holding timestamps (of a writer
+        # zone other than UTC: the GPU path decodes UTC writers only)
+        root = reader.types[0]
+        for n, s in zip(root.field_names, root.subtypes):
+            assert n in fields or _has_timestamp(reader, s), "%s: field %s was not decoded" % (where, n)
     if fields is None and 0 not in batch.columns:
         return None  # a non-struct root the GPU path does not decode (a non-UTC timestamp)
     got = batch.to_pylist(fields)
