@@ -49,7 +49,15 @@ typedef struct orcg_ctx orcg_ctx;
 int orcg_ctx_create(int device, orcg_ctx** out);
 void orcg_ctx_destroy(orcg_ctx* ctx);
 /* Use an external stream (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+ * NULL restores the context's own stream.
+ * Ordering contract of every *_device entry: the launch is queued on the
+ * context stream and nothing else. The context's own stream is
+ * non-blocking, so it is NOT ordered after work on the legacy NULL stream or
+ * any other stream: a caller that fills or copies d_src / d_segs / d_dst on
+ * stream P must either pass P here, or make the context stream wait on an
+ * event recorded on P (hipStreamWaitEvent(orcg_ctx_stream(ctx), ev, 0))
+ * before the call. Consumers of d_dst order after the context stream the
+ * same way (tests/test_gpu_stream_order.py). */
 int orcg_ctx_set_stream(orcg_ctx* ctx, void* hip_stream);
 void* orcg_ctx_stream(orcg_ctx* ctx);
 /* Wait for the context stream and collect any device-side decode error of

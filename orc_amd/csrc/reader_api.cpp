@@ -1503,6 +1503,10 @@ struct orcg_row_reader {
   std::condition_variable cv;
   std::deque<uint64_t> jobs;
   bool stop = false;
+  // the worker's own context (stream, error record, scratch, queues): the
+  // caller's context may be driven by its thread while the worker decodes
+  // ahead, e.g. by another reader sharing it
+  orcg_ctx* own = nullptr;
 
   ~orcg_row_reader() {
     {
@@ -1512,6 +1516,7 @@ struct orcg_row_reader {
     }
     cv.notify_all();
     if (worker.joinable()) worker.join();
+    if (own) orcg_ctx_destroy(own);
   }
 
   void mark_end_of_file() {
@@ -1522,19 +1527,24 @@ struct orcg_row_reader {
   }
 
   // --- worker side -------------------------------------------------------
-  struct OptsSwap {  // this row reader's options on the reader for one decode
+  struct OptsSwap {  // this row reader's options and context on the reader for one decode
     // (copied, not swapped: the caller thread reads the row reader's own
     // selection meanwhile)
     orcg_reader* r;
     std::vector<uint8_t> sel;
     bool lazy;
-    OptsSwap(orcg_reader* r_, const orcg_row_reader* rr) : r(r_), sel(r_->selected), lazy(r_->lazy_dict) {
+    Ctx* ctx;
+    OptsSwap(orcg_reader* r_, const orcg_row_reader* rr)
+        : r(r_), sel(r_->selected), lazy(r_->lazy_dict), ctx(r_->ctx) {
       r->selected = rr->selected;
       r->lazy_dict = rr->lazy_dict;
+      rr->own->rlev2_variant = ctx->rlev2_variant;  // the caller's kernel choice
+      r->ctx = rr->own;
     }
     ~OptsSwap() {
       r->selected.swap(sel);
       r->lazy_dict = lazy;
+      r->ctx = ctx;
     }
   };
   // D2H of every decoded column of `dev` into the slab (one synchronisation)
@@ -1955,6 +1965,8 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
   int rc = compute_selection(r, o ? o->include : nullptr, o && o->include ? o->include_len : 0, rr->selected);
   if (rc) return rc;
   rr->lazy_dict = o && o->lazy_dictionary != 0;
+  if ((rc = orcg_ctx_create(r->ctx->device, &rr->own)) != ORCG_OK)
+    return r->fail(rc, "row reader context creation failed");
   const uint64_t ns = r->footer.stripes.size();
   rr->nstripes = ns;
   rr->current = ns;
