@@ -97,7 +97,7 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
 
 // RLEv2 kernel variants a context accepts (orcg_rlev2_variants): 0 default,
 // 1 wave-walk, and pins of single tiled instances (launch_rlev2_tiled).
-constexpr int kMaxRlev2Variant = 35;
+constexpr int kMaxRlev2Variant = 39;
 bool rlev2_variant_valid(int v);
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,

@@ -98,6 +98,8 @@ constexpr int kOptScan = 4096;      // dense discovery: block entries by a wave 
                                     // no LDS gathers), the pointer-doubling chain only when a run jumps too far
 constexpr int kOptPrefetch = 2048;  // register-filled serial windows: every wave loads its share of the next window
                                     // into registers as soon as the walk is done, while it expands this one
+constexpr int kOptGrpT = 8192;      // serial groups of short runs (one lane per run, scattered 8-byte stores):
+                                    // temporal stores, so L2 merges the partial lines before they reach HBM
 
 // Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
 // counts the values of the runs it expands; each pass checks the count
@@ -734,6 +736,7 @@ template <int kOpt, typename T, typename OffT>
 __device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_off, const uint32_t* s_val,
                                              uint32_t r0, uint32_t r1, uint64_t vi, int is_signed,
                                              uint64_t value_begin, uint64_t value_end, T* dst, int lane) {
+  constexpr int kGrpOpt = (kOpt & kOptGrpT) != 0 ? (kOpt & ~kOptNTStore) : kOpt;
   const uint32_t r = r0 + (uint32_t)lane;
   const bool act = r < r1;
   const uint32_t hoff = act ? s_off[r] : s_off[r0];
@@ -754,7 +757,7 @@ __device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_
     ORCG_COVER_ADD(L);
     for (uint32_t j = 0; __ballot(j < L) != 0; ++j) {
       const uint64_t o = o0 + j;
-      if (j < L && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), a);
+      if (j < L && o >= value_begin && o < value_end) store1<kGrpOpt>(dst + (o - value_begin), a);
     }
     return;
   }
@@ -766,7 +769,7 @@ __device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_
     const uint64_t o = o0 + j;
     if (j < L) {
       const uint64_t x = short_value(win, run, hoff, j, is_signed, acc);
-      if (o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), x);
+      if (o >= value_begin && o < value_end) store1<kGrpOpt>(dst + (o - value_begin), x);
     }
   }
 }
@@ -2278,6 +2281,10 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     case 33: ORCG_KT(kWide | kOptPrefetch, 16, false, 5, false); break;               // 16 KB + prefetch, 5 WG/CU
     case 34: ORCG_KT(kSer | kOptD3 | kOptUnion | kOptScan, 8, false, 6, 2); break;      // union + scan chain
     case 35: ORCG_KT(kSer | kOptD3 | kOptScan, 8, false, 6, 2); break;                  // dense v3 (4) + scan chain
+    case 36: ORCG_KT(kWide | kOptD3 | kOptPair, 33, false, 1, 0); break;                 // 2 + 16-byte pair stores
+    case 37: ORCG_KT((kWide & ~kOptNTStore) | kOptD3, 33, false, 1, 0); break;          // 2 with plain (temporal) stores
+    case 38: ORCG_KT(kWide | kOptD3 | kOptGrpT, 33, false, 1, 0); break;                 // 2 + temporal short-run group stores
+    case 39: ORCG_KT(kSer | kOptGrpT, 21, false, 6, false); break;                       // 16 + temporal short-run group stores
 #endif
     default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "unknown RLEv2 kernel variant");
   }
