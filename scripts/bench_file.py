@@ -113,7 +113,7 @@ def concat_leg(dist, r, path, first, last, rank):
 
 def row_reader_leg(path, nrows, stripes_wall):
     """The reference caller's path: orc::RowReader::next(batch) at capacity
-    1024 through the C++ adapter (orc_amd/csrc/GpuRowReader.hh), every batch
+    1024 (the reference's default batch) and 16384 through the C++ adapter (orc_amd/csrc/GpuRowReader.hh), every batch
     filled into host ColumnVectorBatches; a compiled program
     (tests/cxx/reader_test.cpp --bench), timed from the first next() to the
     last."""
@@ -128,7 +128,7 @@ def row_reader_leg(path, nrows, stripes_wall):
                                exe, "-L" + os.path.join(ROOT, "orc_amd"), "-lorcgpu",
                                "-Wl,-rpath," + os.path.join(ROOT, "orc_amd"), "-Wl,-rpath,/opt/rocm/lib"])
     out = {}
-    for cap in (1024,):
+    for cap in (1024, 16384):
         r = subprocess.run([exe, path, "--bench", "--batch", str(cap)], capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             raise SystemExit("row reader bench failed: %s" % r.stderr[-500:])
