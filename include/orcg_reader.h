@@ -198,6 +198,10 @@ uint64_t orcg_row_reader_row_number(const orcg_row_reader* rr);
 uint64_t orcg_row_reader_stripe(const orcg_row_reader* rr);
 /* RowReader::seekToRow: the next batch starts at `row` */
 int orcg_row_reader_seek_to_row(orcg_row_reader* rr, uint64_t row);
+/* this row reader's last failure (a prefetched stripe's error, surfaced by
+ * next / seek); the reader's orcg_reader_last_error also carries it, but is
+ * shared with every row reader of that reader */
+const char* orcg_row_reader_last_error(const orcg_row_reader* rr);
 /* the last batch's view of column type_id (host pointers, see above) */
 int orcg_row_reader_column(const orcg_row_reader* rr, uint32_t type_id, orcg_column_view* view, uint64_t* begin,
                            uint64_t* count);

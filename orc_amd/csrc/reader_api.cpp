@@ -260,20 +260,39 @@ struct orcg_reader {
   // serialises decodes: the reader's own reads and the row readers' prefetch
   // workers share its decode state (stages, batch tables, checks)
   std::mutex mu;
+  // The reader's own options: its context (fixed at open), its column
+  // selection and lazy-dictionary flag (changed under mu). Entry points that
+  // run outside a decode (copy_to_host, is_selected, row reader creation)
+  // read only these; a row reader's worker never writes them.
+  Ctx* own_ctx = nullptr;
+  std::vector<uint8_t> own_sel;  // per type id
+  bool own_lazy = false;
+  // The options of the decode in progress (valid under mu, set by Active):
+  // the reader's own for its reads, a row reader's for that row reader's
+  // prefetch decodes.
   Ctx* ctx = nullptr;
+  std::vector<uint8_t> selected;
+  bool lazy_dict = false;
+  struct Active {
+    orcg_reader* r;
+    Active(orcg_reader* r_, Ctx* c, const std::vector<uint8_t>& sel, bool lazy) : r(r_) {
+      r->ctx = c;
+      r->selected = sel;
+      r->lazy_dict = lazy;
+    }
+    ~Active() { r->ctx = nullptr; }
+  };
   const uint8_t* file = nullptr;
   uint64_t file_len = 0;
   void* mapped = nullptr;
   PostScript ps;
   Footer footer;
-  std::vector<uint8_t> selected;  // per type id
   std::string last_error;
   HostStage stages[2];
   bool decimal_as_long = false;  // PostScript version 1.9999 (UNSTABLE-PRE-2.0): Decimal64V2 columns (Reader.cc:1693-1699)
-  bool lazy_dict = false;
   int32_t hive11_scale = 6;  // RowReaderOptions::forcedScaleOnHive11Decimal (Reader.cc RowReaderOptionsPrivate: 6)
   bool hive11_throw = true;  // RowReaderOptions::throwOnHive11DecimalOverflow (default true)
-  std::string software_version;  // orcg_reader_software_version's buffer  // RowReaderOptions::setEnableLazyDecoding: dictionary columns keep index + dictionary only
+  std::string software_version;  // orcg_reader_software_version's buffer
   std::vector<std::unique_ptr<DevSlot>> slots;  // results of the last read, in stripe order
   size_t nslots = 0;
   // decode() state: the host stage and device slot of the stripe being decoded
@@ -317,6 +336,14 @@ struct orcg_reader {
     return status;
   }
   int fail_ctx(int rc) { return fail(rc, ctx ? ctx->last_error : std::string("device error")); }
+  // a failure outside a decode (argument checks of the caller's thread):
+  // last_error is shared with the row readers' workers, so under mu
+  int fail_user(int status, const std::string& m) {
+    std::lock_guard<std::mutex> lk(mu);
+    last_error = m;
+    if (own_ctx) own_ctx->last_error = m;
+    return status;
+  }
   int fail_oom(int line) {
     static const bool dbg = getenv("ORCG_DEBUG_ALLOC") != nullptr;
     if (dbg) fprintf(stderr, "orcg: reader device allocation failed at reader_api.cpp:%d (column %u)\n", line, cur_col);
@@ -404,7 +431,7 @@ int orcg_reader::open_tail() {
                                           std::to_string(j) + ") in types(" + std::to_string(i) + ")");
     }
   }
-  selected.assign(nt, 1);
+  own_sel.assign(nt, 1);
   return ORCG_OK;
 }
 
@@ -1251,12 +1278,17 @@ int orcg_reader::first_error(int inline_rc) {
   if (nc && hipMemcpy(rec.data(), D->d_errs, 8 * nc, hipMemcpyDeviceToHost) != hipSuccess)
     return fail(ORCG_DEVICE_ERROR, "read error records");
   const uint32_t last = inline_rc ? (inline_col == kNoCol ? 0u : inline_col) : (uint32_t)nc;
+  // checks grouped by column once (stable: a column's checks keep their
+  // order), then one walk over columns and checks together
+  std::stable_sort(checks.begin(), checks.end(),
+                   [](const std::pair<uint32_t, std::function<int()>>& a,
+                      const std::pair<uint32_t, std::function<int()>>& b) { return a.first < b.first; });
+  size_t ci = 0;
   for (uint32_t col = 0; col < nc && col <= last; ++col) {
-    for (auto& ch : checks)
-      if (ch.first == col) {
-        const int rc = ch.second();
-        if (rc) return rc;
-      }
+    for (; ci < checks.size() && checks[ci].first <= col; ++ci) {
+      const int rc = checks[ci].second();
+      if (rc) return rc;
+    }
     if (rec[col] != kNoError) {
       const uint32_t code = (uint32_t)(rec[col] & 0xff);
       ctx->last_error_value = rec[col] >> 8;
@@ -1501,6 +1533,7 @@ struct orcg_row_reader {
   std::thread worker;
   std::mutex m;
   std::condition_variable cv;
+  std::string last_error;  // this row reader's last failure (orcg_row_reader_last_error)
   std::deque<uint64_t> jobs;
   bool stop = false;
   // the worker's own context (stream, error record, scratch, queues): the
@@ -1527,26 +1560,9 @@ struct orcg_row_reader {
   }
 
   // --- worker side -------------------------------------------------------
-  struct OptsSwap {  // this row reader's options and context on the reader for one decode
-    // (copied, not swapped: the caller thread reads the row reader's own
-    // selection meanwhile)
-    orcg_reader* r;
-    std::vector<uint8_t> sel;
-    bool lazy;
-    Ctx* ctx;
-    OptsSwap(orcg_reader* r_, const orcg_row_reader* rr)
-        : r(r_), sel(r_->selected), lazy(r_->lazy_dict), ctx(r_->ctx) {
-      r->selected = rr->selected;
-      r->lazy_dict = rr->lazy_dict;
-      rr->own->rlev2_variant = ctx->rlev2_variant;  // the caller's kernel choice
-      r->ctx = rr->own;
-    }
-    ~OptsSwap() {
-      r->selected.swap(sel);
-      r->lazy_dict = lazy;
-      r->ctx = ctx;
-    }
-  };
+  // (every decode runs under r->mu with this row reader's options and
+  // context as the reader's active ones, orcg_reader::Active; the reader's
+  // own options are never touched)
   // D2H of every decoded column of `dev` into the slab (one synchronisation)
   int copy_out(HostSlab& sl) {
     sl.out = dev->out;
@@ -1591,7 +1607,7 @@ struct orcg_row_reader {
     std::string err;
     {
       std::lock_guard<std::mutex> lk(r->mu);
-      OptsSwap sw(r, this);
+      orcg_reader::Active act(r, own, selected, lazy_dict);
       (void)hipSetDevice(r->ctx->device);
       rc = ORCG_OK;
       if (prepared[t & 1] != t) {
@@ -1626,7 +1642,7 @@ struct orcg_row_reader {
       }
       if (idle) {
         std::lock_guard<std::mutex> lk(r->mu);
-        OptsSwap sw(r, this);
+        orcg_reader::Active act(r, own, selected, lazy_dict);
         prepared[u & 1] = u;
         (void)r->prepare(u, stage[u & 1]);  // a failure is kept in the stage
       }
@@ -1667,7 +1683,10 @@ struct orcg_row_reader {
     cv.wait(lk, [&] { return slab_state[s & 1] == 2; });
     if (sl.rc) {
       const int rc = sl.rc;
-      r->last_error = sl.err;
+      last_error = sl.err;
+      lk.unlock();
+      r->fail_user(rc, sl.err);  // also the reader's (its workers write it under r->mu)
+      lk.lock();
       slab_state[s & 1] = 0;  // a later seek decodes it again
       cur = nullptr;
       return rc;
@@ -1718,7 +1737,7 @@ int orcg_reader_open(orcg_ctx* ctx, const uint8_t* file, uint64_t file_len, orcg
   if (!out || (file_len && !file)) return ORCG_INVALID_ARGUMENT;
   *out = nullptr;
   std::unique_ptr<orcg_reader> r(new orcg_reader());
-  r->ctx = ctx;
+  r->own_ctx = ctx;
   r->file = file;
   r->file_len = file_len;
   const int rc = r->open_tail();
@@ -1751,7 +1770,7 @@ int orcg_reader_open_file(orcg_ctx* ctx, const char* path, orcg_reader** out) {
     return ORCG_INVALID_ARGUMENT;
   }
   std::unique_ptr<orcg_reader> r(new orcg_reader());
-  r->ctx = ctx;
+  r->own_ctx = ctx;
   r->file = (const uint8_t*)m;
   r->file_len = len;
   r->mapped = m;
@@ -1795,7 +1814,7 @@ const uint8_t* orcg_reader_metadata_value(const orcg_reader* r, uint32_t i, uint
 int orcg_reader_set_lazy_dictionary(orcg_reader* r, int on) {
   if (!r) return ORCG_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(r->mu);
-  r->lazy_dict = on != 0;
+  r->own_lazy = on != 0;
   return ORCG_OK;
 }
 int orcg_reader_set_hive11_decimal(orcg_reader* r, int32_t forced_scale, int throw_on_overflow) {
@@ -1851,7 +1870,7 @@ static int compute_selection(orcg_reader* r, const uint8_t* include, uint32_t nt
   const size_t nt = r->footer.types.size();
   sel.assign(nt, 1);
   if (!include) return ORCG_OK;
-  if (ntypes > nt) return r->fail(ORCG_INVALID_ARGUMENT, "include list longer than the type list");
+  if (ntypes > nt) return r->fail_user(ORCG_INVALID_ARGUMENT, "include list longer than the type list");
   std::vector<uint32_t> parent(nt, 0);
   for (size_t i = 0; i < nt; ++i)
     for (uint32_t st : r->footer.types[i].subtypes) parent[st] = (uint32_t)i;
@@ -1877,23 +1896,25 @@ int orcg_reader_select(orcg_reader* r, const uint8_t* include, uint32_t ntypes) 
   const int rc = compute_selection(r, include, ntypes, sel);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(r->mu);
-  r->selected.swap(sel);
+  r->own_sel.swap(sel);
   return ORCG_OK;
 }
 
 int orcg_reader_is_selected(const orcg_reader* r, uint32_t type_id) {
-  return r && type_id < r->selected.size() && r->selected[type_id] ? 1 : 0;
+  return r && type_id < r->own_sel.size() && r->own_sel[type_id] ? 1 : 0;
 }
 
 int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe) {
   if (!r) return ORCG_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(r->mu);
+  orcg_reader::Active act(r, r->own_ctx, r->own_sel, r->own_lazy);
   return r->read_stripes(stripe, 1);
 }
 
 int orcg_reader_bench_stripe_decode(orcg_reader* r, uint64_t stripe, uint32_t iters, double* decode_s, double* h2d_s) {
   if (!r || !decode_s || !h2d_s || iters == 0) return ORCG_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(r->mu);
+  orcg_reader::Active act(r, r->own_ctx, r->own_sel, r->own_lazy);
   if (!r->ctx) return r->fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
   if (stripe >= r->footer.stripes.size()) return r->fail(ORCG_INVALID_ARGUMENT, "stripe index out of range");
   hipSetDevice(r->ctx->device);
@@ -1914,6 +1935,7 @@ int orcg_reader_bench_stripe_decode(orcg_reader* r, uint64_t stripe, uint32_t it
 int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count) {
   if (!r) return ORCG_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(r->mu);
+  orcg_reader::Active act(r, r->own_ctx, r->own_sel, r->own_lazy);
   return r->read_stripes(first, count);
 }
 
@@ -1947,17 +1969,18 @@ int orcg_reader_column(const orcg_reader* r, uint32_t id, orcg_column_view* out)
 }
 
 int orcg_reader_copy_to_host(orcg_reader* r, void* dst, const void* src, uint64_t bytes) {
-  if (!r || !r->ctx || (bytes && (!dst || !src))) return ORCG_INVALID_ARGUMENT;
+  if (!r || !r->own_ctx || (bytes && (!dst || !src))) return ORCG_INVALID_ARGUMENT;
   if (!bytes) return ORCG_OK;
-  int rc = hip_check(r->ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, r->ctx->stream), "D2H");
-  if (!rc) rc = sync_ctx(r->ctx);
+  Ctx* c = r->own_ctx;  // never a row reader worker's context
+  int rc = hip_check(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream), "D2H");
+  if (!rc) rc = sync_ctx(c);
   return rc;
 }
 
 int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orcg_row_reader** out) {
   if (!r || !out) return ORCG_INVALID_ARGUMENT;
   *out = nullptr;
-  if (!r->ctx) return r->fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
+  if (!r->own_ctx) return r->fail_user(ORCG_INVALID_ARGUMENT, "reader has no device context");
   const uint64_t off = o ? o->offset : 0;
   const uint64_t len = o ? o->length : ~0ull;
   std::unique_ptr<orcg_row_reader> rr(new orcg_row_reader());
@@ -1965,8 +1988,11 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
   int rc = compute_selection(r, o ? o->include : nullptr, o && o->include ? o->include_len : 0, rr->selected);
   if (rc) return rc;
   rr->lazy_dict = o && o->lazy_dictionary != 0;
-  if ((rc = orcg_ctx_create(r->ctx->device, &rr->own)) != ORCG_OK)
-    return r->fail(rc, "row reader context creation failed");
+  if ((rc = orcg_ctx_create(r->own_ctx->device, &rr->own)) != ORCG_OK)
+    return r->fail_user(rc, "row reader context creation failed");
+  // the caller's kernel choice, snapshotted once: the worker never reads the
+  // caller's context
+  rr->own->rlev2_variant = r->own_ctx->rlev2_variant;
   const uint64_t ns = r->footer.stripes.size();
   rr->nstripes = ns;
   rr->current = ns;
@@ -2036,6 +2062,8 @@ int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows)
 }
 
 uint64_t orcg_row_reader_row_number(const orcg_row_reader* rr) { return rr ? rr->previous_row : 0; }
+
+const char* orcg_row_reader_last_error(const orcg_row_reader* rr) { return rr ? rr->last_error.c_str() : "null row reader"; }
 
 uint64_t orcg_row_reader_stripe(const orcg_row_reader* rr) { return rr ? rr->batch_stripe : ~0ull; }
 

@@ -91,7 +91,6 @@ constexpr int kOptT4 = 32;
 constexpr int kOptD3 = 64;      // dense discovery: predicated chain marks, wave-reduced control atomics, inline probe
 constexpr int kOptDirect = 128; // dense expansion: lanes store their short runs' values straight to the output (no stage)
 constexpr int kOptPair = 256;   // full DIRECT runs: two values per lane, one 16-byte store (16-byte aligned int64 output)
-constexpr int kOptVP = 512;     // serial groups of short runs expanded value-parallel (coalesced stores)
 constexpr int kOptUnion = 1024; // dense v2 instance whose serial (long-run) windows also cover the dense stage and
                                 // marks: one instance routes each window by its runs (dense or serial), no queue
 constexpr int kOptScan = 4096;      // dense discovery: block entries by a wave scan of entry-state functions (DPP,
@@ -772,63 +771,6 @@ __device__ __forceinline__ void group_expand(const uint32_t* win, const OffT* s_
       if (o >= value_begin && o < value_end) store1<kGrpOpt>(dst + (o - value_begin), x);
     }
   }
-}
-
-// Expand runs [r0, r1) (<= 64 short SHORT_REPEAT / DIRECT / fixed-delta runs)
-// value-parallel: lane k parses run r0 + k, a wave scan of the run lengths
-// gives each run's first value in the group, then lane t of every 64-value
-// chunk finds its run by a binary search over the lanes (ds_bpermute) and
-// extracts its value, so each store instruction writes 64 consecutive values
-// (one lane per run scatters every store over up to 64 cache lines). Returns
-// false, having done nothing, when the group holds a run it does not handle
-// (PATCHED_BASE, variable-width DELTA).
-template <int kOpt, typename T, typename OffT>
-__device__ __forceinline__ bool group_expand_vp(const uint32_t* win, const OffT* s_off, const uint32_t* s_val,
-                                                uint32_t r0, uint32_t r1, uint64_t vi, int is_signed,
-                                                uint64_t value_begin, uint64_t value_end, T* dst, int lane) {
-  const uint32_t n = r1 - r0;
-  const uint32_t r = r0 + (uint32_t)lane;
-  const bool act = r < r1;
-  const uint32_t hoff = act ? s_off[r] : s_off[r0];
-  const Run run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
-  if (__ballot(act && (run.kind == 2 || (run.kind == 3 && run.W != 0))) != 0) return false;
-  ORCG_COVER_ADD(act ? run.L : 0u);
-  const uint32_t L = act ? run.L : 0u;
-  const uint32_t incl = wave_scan_u32(L);
-  const uint32_t st = incl - L;  // the run's first value in the group
-  const uint32_t total = rdlane(incl, 63);
-  const uint32_t kw = act ? (run.kind | (run.W << 8)) : 0u;
-  const uint32_t db = hoff + run.data;
-  const uint64_t o0 = vi + uni(s_val[r0]);
-  auto perm = [](uint32_t v, uint32_t src) -> uint32_t {
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
-  };
-  for (uint32_t t0 = 0; t0 < total; t0 += kWave) {
-    const uint32_t t = t0 + (uint32_t)lane;
-    // the last run whose first value is <= t (runs of >= 1 value: it holds t)
-    uint32_t k = 0;
-#pragma unroll
-    for (uint32_t step = 32; step >= 1; step >>= 1)
-      if (k + step < n && perm(st, k + step) <= t) k += step;
-    const uint32_t kwk = perm(kw, k), kind = kwk & 0xffu, W = kwk >> 8;
-    const uint32_t j = t - perm(st, k);
-    const uint64_t a = ((uint64_t)perm((uint32_t)(run.a >> 32), k) << 32) | perm((uint32_t)run.a, k);
-    uint64_t v;
-    if (kind == 1) {
-      const uint32_t bit = j * W;
-      const uint32_t br = perm(db, k) + (bit >> 3);
-      v = field(lds12(win, br), br, bit & 7u, W);
-      if (is_signed) v = unzigzag(v);
-    } else if (kind == 3) {
-      const uint64_t b = ((uint64_t)perm((uint32_t)(run.b >> 32), k) << 32) | perm((uint32_t)run.b, k);
-      v = a + (uint64_t)j * b;
-    } else {
-      v = a;
-    }
-    const uint64_t o = o0 + t;
-    if (t < total && o >= value_begin && o < value_end) store1<kOpt>(dst + (o - value_begin), v);
-  }
-  return true;
 }
 
 // ---- dense mode -----------------------------------------------------------
@@ -1954,9 +1896,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               // coalesced stores through the wave's value stage
               dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], s_stage2 + wave * kStage, r0, e, vi,
                                  is_signed, value_begin, value_end, dst, lane);
-            else if (!((kOpt & kOptVP) != 0 &&
-                       group_expand_vp<kOpt>(s_win[0], s_off[0], s_val[0], r0, e, vi, is_signed, value_begin,
-                                             value_end, dst, lane)))
+            else
               group_expand<kOpt>(s_win[0], s_off[0], s_val[0], r0, e, vi, is_signed, value_begin, value_end, dst,
                                  lane);
           }

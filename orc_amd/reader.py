@@ -499,6 +499,9 @@ class RowReader:
         self._dicts = {}  # the current stripe's dictionaries (host copies)
         self._dict_stripe = None
 
+    def _err(self):
+        return self._L.orcg_row_reader_last_error(self._h)
+
     def is_selected(self, tid):
         """RowReader::getSelectedColumns()[tid]."""
         return bool(self._L.orcg_row_reader_is_selected(self._h, tid))
@@ -517,7 +520,7 @@ class RowReader:
     def next(self, batch):
         """RowReader::next: True with batch.num_elements rows, False at the end."""
         rows = ctypes.c_uint64()
-        check(self._L.orcg_row_reader_next(self._h, batch.capacity, ctypes.byref(rows)), self.reader._err)
+        check(self._L.orcg_row_reader_next(self._h, batch.capacity, ctypes.byref(rows)), self._err)
         batch.num_elements = rows.value
         batch.columns = {}
         if rows.value == 0:
@@ -558,7 +561,7 @@ class RowReader:
 
     def seek_to_row(self, row):
         """RowReader::seekToRow: the next batch starts at `row`."""
-        check(self._L.orcg_row_reader_seek_to_row(self._h, int(row)), self.reader._err)
+        check(self._L.orcg_row_reader_seek_to_row(self._h, int(row)), self._err)
 
 
 def open_reader(source, ctx=None, device=True):

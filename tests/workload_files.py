@@ -60,7 +60,7 @@ def _dict_strings(pa, rng, words, n):
     return pa.DictionaryArray.from_arrays(idx, pa.array(words)).cast(pa.string())
 
 
-def make_c4(path, rows, stripe_mb, row_index_stride=10000):
+def make_c4(path, rows, stripe_mb, row_index_stride=10000, compression="zstd"):
     import pyarrow as pa
     import pyarrow.compute as pc
     import pyarrow.orc as po
@@ -96,11 +96,11 @@ def make_c4(path, rows, stripe_mb, row_index_stride=10000):
         "l_shipmode": _dict_strings(pa, rng, ["REG AIR", "AIR", "RAIL", "SHIP", "TRUCK", "MAIL", "FOB"], rows),
         "l_comment": pc.binary_join_element_wise(c1, c2, " "),
     })
-    po.write_table(table, path, compression="zstd", stripe_size=stripe_mb << 20,
+    po.write_table(table, path, compression=compression, stripe_size=stripe_mb << 20,
                    dictionary_key_size_threshold=0.5, row_index_stride=row_index_stride)
 
 
-def make_c5(path, rows, stripe_mb, row_index_stride=10000):
+def make_c5(path, rows, stripe_mb, row_index_stride=10000, compression="zstd"):
     import pyarrow as pa
     import pyarrow.orc as po
 
@@ -124,5 +124,5 @@ def make_c5(path, rows, stripe_mb, row_index_stride=10000):
     items = pa.array(rng.integers(0, 1 << 20, size=nm).astype(np.int32), mask=rng.random(nm) < 0.1)
     m = pa.MapArray.from_arrays(pa.array(off_m), keys, items, mask=pa.array(null_m))
     s = pa.StructArray.from_arrays([a, m], names=["a", "m"], mask=pa.array(rng.random(rows) < 0.1))
-    po.write_table(pa.table({"s": s}), path, compression="zstd", stripe_size=stripe_mb << 20,
+    po.write_table(pa.table({"s": s}), path, compression=compression, stripe_size=stripe_mb << 20,
                    dictionary_key_size_threshold=1.0, row_index_stride=row_index_stride)
