@@ -196,14 +196,14 @@ int orcg_byterle_decode_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_l
                                uint64_t nsegs, uint64_t value_begin, uint64_t nvalues, uint8_t* d_dst) {
   if (!c || (nsegs && (!d_src || !d_segs)) || (nvalues && !d_dst)) return ORCG_INVALID_ARGUMENT;
   (void)hipSetDevice(c->device);
-  return launch_byterle(c, d_src, src_len, (const uint64_t*)d_segs, nsegs, false, value_begin, nvalues, d_dst);
+  return launch_byterle(c, d_src, src_len, (const uint64_t*)d_segs, nsegs, false, value_begin, nvalues, d_dst, nullptr);
 }
 
 int orcg_boolrle_decode_device(orcg_ctx* c, const uint8_t* d_src, uint64_t src_len, const orcg_segment* d_segs,
                                uint64_t nsegs, uint64_t row_begin, uint64_t nrows, uint8_t* d_dst) {
   if (!c || (nsegs && (!d_src || !d_segs)) || (nrows && !d_dst)) return ORCG_INVALID_ARGUMENT;
   (void)hipSetDevice(c->device);
-  return launch_byterle(c, d_src, src_len, (const uint64_t*)d_segs, nsegs, true, row_begin, nrows, d_dst);
+  return launch_byterle(c, d_src, src_len, (const uint64_t*)d_segs, nsegs, true, row_begin, nrows, d_dst, nullptr);
 }
 
 int orcg_byte_rle_decoder_create(orcg_ctx* c, const uint8_t* src, uint64_t len, int boolean,

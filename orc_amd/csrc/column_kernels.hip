@@ -281,7 +281,20 @@ __global__ __launch_bounds__(kThreads) void rg_count_kernel(const uint8_t* __res
   if (a > n) a = n;
   if (b > n) b = n;
   uint32_t c = 0;
-  for (uint64_t r = a + threadIdx.x; r < b; r += kThreads) c += mask[r] != 0;
+  if (b > a) {
+    // 16-byte loads over the aligned middle, bytes at the two ends
+    const uintptr_t pa = (uintptr_t)(mask + a), pb = (uintptr_t)(mask + b);
+    const uintptr_t ma = (pa + 15) & ~(uintptr_t)15, mb = pb & ~(uintptr_t)15;
+    if (ma < mb) {
+      const u4* v = (const u4*)ma;
+      const uint64_t nv = (uint64_t)(mb - ma) / 16;
+      for (uint64_t k = threadIdx.x; k < nv; k += kThreads) c += nn_bytes_count(v[k]);
+      for (uintptr_t q = pa + threadIdx.x; q < ma; q += kThreads) c += *(const uint8_t*)q != 0;
+      for (uintptr_t q = mb + threadIdx.x; q < pb; q += kThreads) c += *(const uint8_t*)q != 0;
+    } else {
+      for (uint64_t r = a + threadIdx.x; r < b; r += kThreads) c += mask[r] != 0;
+    }
+  }
   for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor((int)c, m);
   if (threadIdx.x % kWave == 0) red[threadIdx.x / kWave] = c;
   __syncthreads();

@@ -111,8 +111,10 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs);
 // Variants whose instances take job tables with row-index segments (RleJob::trip).
 bool rlev2_multi_capable(int variant);
 
+// d_ones (boolean mode, may be null): += the set rows written (a PRESENT
+// stream's non-null rows), one atomic per wave
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
-                   bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst);
+                   bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst, uint64_t* d_ones = nullptr);
 int launch_rlev1(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed, const uint64_t* d_segtab,
                  uint64_t nsegs, uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes);
 int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,

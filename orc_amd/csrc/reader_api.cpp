@@ -253,6 +253,7 @@ struct DevSlot {
   uint8_t* d_stage = nullptr;
   uint64_t* d_scalars = nullptr;
   unsigned long long* d_errs = nullptr;  // device error record per column (the kernels' atomicMin word)
+  uint64_t* d_ones = nullptr;            // per column: non-null rows its PRESENT decode wrote
   std::vector<ColOut> out;
 };
 
@@ -324,10 +325,36 @@ struct orcg_reader {
     return h;
   }
 
+  // Mid-stripe reads the host must wait for (list / map totals, union
+  // counts): 8-byte D2H copies into pinned memory (one DMA each; a pageable
+  // destination costs two staging copies), then one stream synchronisation.
+  uint64_t* h_sync = nullptr;
+  size_t sync_cap = 0;
+  int read_back(const std::vector<const void*>& src, uint64_t* out) {
+    if (src.size() > sync_cap) {
+      if (h_sync) (void)hipHostFree(h_sync);
+      h_sync = nullptr;
+      sync_cap = 0;
+      const size_t cap = std::max<size_t>(64, src.size());
+      if (hipHostMalloc((void**)&h_sync, cap * 8, hipHostMallocDefault) != hipSuccess)
+        return fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed");
+      sync_cap = cap;
+    }
+    for (size_t i = 0; i < src.size(); ++i) {
+      const int rc = hip_check(ctx, hipMemcpyAsync(h_sync + i, src[i], 8, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+      if (rc) return fail_ctx(rc);
+    }
+    const int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
+    if (rc) return fail_ctx(rc);
+    for (size_t i = 0; i < src.size(); ++i) out[i] = h_sync[i];
+    return ORCG_OK;
+  }
+
   ~orcg_reader() {
     slots.clear();
     if (mapped) munmap(mapped, file_len);
     if (h_defer) (void)hipHostFree(h_defer);
+    if (h_sync) (void)hipHostFree(h_sync);
   }
   int fail(int status, const std::string& m) {
     if (err_col == kNoCol) err_col = cur_col;
@@ -376,8 +403,7 @@ struct orcg_reader {
   std::unordered_map<uint64_t, std::pair<int64_t*, uint64_t>> batched;  // (column, slot) -> (values, count)
   int queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2);
   int collect(uint32_t id, uint64_t n, const int64_t* rg_rows);
-  int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out);
-  int nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out);
+  int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones = nullptr);
   int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
   template <typename T>
   T* alloc(uint64_t count) {
@@ -433,15 +459,6 @@ int orcg_reader::open_tail() {
   }
   own_sel.assign(nt, 1);
   return ORCG_OK;
-}
-
-int orcg_reader::nonnull_count(const uint8_t* nn, uint64_t n, uint64_t& out) {
-  int rc = launch_count_nonzero(ctx, nn, n, D->d_scalars);
-  if (!rc) rc = hip_check(ctx, hipMemcpyAsync(&out, D->d_scalars, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H count");
-  // a stream synchronisation only: the columns' device error records are
-  // read once, at the end of the stripe (first_error)
-  if (!rc) rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize");
-  return rc;
 }
 
 int orcg_reader::scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width) {
@@ -589,7 +606,7 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
   return rc;
 }
 
-int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out) {
+int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones) {
   StreamBuf& sb = c.s[slot];
   if (count == 0) return ORCG_OK;
   if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
@@ -604,7 +621,7 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   uint64_t nseg;
   int rc = segments(c, slot, boolean, &d_seg, &nseg);
   if (rc) return rc;
-  rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out);
+  rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones);
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
 
@@ -636,14 +653,17 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   uint8_t* nn = nullptr;
   if (c.s[kSlotPresent].present) {
     ORCG_ALLOC(uint8_t, bits, in_count + 8);
-    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits))) return rc;
+    // the decode counts the set rows it writes: the non-null rows, with or
+    // without the parent's mask scattered in
+    uint64_t* ones = D->d_ones + id;
+    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits, ones))) return rc;
     if (in_nn) {
       ORCG_ALLOC_TO(uint8_t, nn, n);
       if ((rc = scatter(bits, in_nn, n, nn, 1))) return fail_ctx(rc);
     } else {
       nn = bits;
     }
-    if ((rc = nonnull_count(nn, n, nonnull))) return fail_ctx(rc);
+    if ((rc = read_back({ones}, &nonnull))) return rc;
   } else if (in_nn) {
     nn = const_cast<uint8_t*>(in_nn);
   }
@@ -875,9 +895,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if ((rc = launch_exclusive_scan(ctx, rlen, n, off))) return fail_ctx(rc);
     c.offsets = off;
     uint64_t total = 0;
-    if ((rc = hip_check(ctx, hipMemcpyAsync(&total, off + n, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
-        (rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize")))
-      return fail_ctx(rc);
+    if ((rc = read_back({off + n}, &total))) return rc;
     // the children's row groups start at the list offsets of the parent's
     int64_t* child_rows = nullptr;
     if (rg_rows && H->ngroups) {
@@ -911,20 +929,19 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       dense_rows = pre;
     }
     std::vector<int64_t*> scans(nch, nullptr);
-    std::vector<uint64_t> counts(nch, 0);
+    std::vector<const void*> rb;  // per child its row count, then the first bad tag
     for (uint32_t kk = 0; kk < nch; ++kk) {
       ORCG_ALLOC_TO(int64_t, scans[kk], nonnull + 1);
       if ((rc = launch_union_flags(ctx, dtags, nonnull, kk, flags)) ||
           (rc = launch_exclusive_scan(ctx, flags, nonnull, scans[kk])) ||
-          (rc = launch_union_offsets(ctx, dtags, nonnull, kk, scans[kk], doffs)) ||
-          (rc = hip_check(ctx, hipMemcpyAsync(&counts[kk], scans[kk] + nonnull, 8, hipMemcpyDeviceToHost,
-                                              ctx->stream), "D2H union count")))
+          (rc = launch_union_offsets(ctx, dtags, nonnull, kk, scans[kk], doffs)))
         return fail_ctx(rc);
+      rb.push_back(scans[kk] + nonnull);
     }
-    uint64_t first_bad = ~0ull;
-    if ((rc = hip_check(ctx, hipMemcpyAsync(&first_bad, bad, 8, hipMemcpyDeviceToHost, ctx->stream), "D2H")) ||
-        (rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "hipStreamSynchronize")))
-      return fail_ctx(rc);
+    rb.push_back(bad);
+    std::vector<uint64_t> counts(nch + 1, 0);
+    if ((rc = read_back(rb, counts.data()))) return rc;
+    const uint64_t first_bad = counts[nch];
     if (first_bad != ~0ull)
       return fail(ORCG_PARSE_ERROR, "Invalid union tag " + std::to_string(first_bad & 0xff) + " for union with " +
                                         std::to_string(nch) + " children");
@@ -1319,10 +1336,12 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   ds.d_stage = (uint8_t*)ds.pool.get(hs.used + 64);
   ds.d_scalars = (uint64_t*)ds.pool.get(64);
   ds.d_errs = (unsigned long long*)ds.pool.get(8 * hs.cols.size() + 8);
-  if (!ds.d_stage || !ds.d_scalars || !ds.d_errs) return fail_oom(__LINE__);
+  ds.d_ones = (uint64_t*)ds.pool.get(8 * hs.cols.size() + 8);
+  if (!ds.d_stage || !ds.d_scalars || !ds.d_errs || !ds.d_ones) return fail_oom(__LINE__);
   stage_bytes += hs.used;
   int rc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, hs.used, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
   if (!rc) rc = hip_check(ctx, hipMemsetAsync(ds.d_errs, 0xff, 8 * hs.cols.size(), ctx->stream), "error records");
+  if (!rc) rc = hip_check(ctx, hipMemsetAsync(ds.d_ones, 0, 8 * hs.cols.size(), ctx->stream), "row counts");
   if (!rc) rc = sync_ctx(ctx);
   if (rc) return fail_ctx(rc);
   const double t1 = now_s();

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--variants", default="0")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--min-bytes", type=int, default=64 << 10, help="skip streams smaller than this")
+    ap.add_argument("--kinds", default="PRESENT,DATA,LENGTH")
+    ap.add_argument("--phases", action="store_true",
+                    help="byte RLE phase split (ORCG_LIB=liborcgpu_prof.so, a -DORCG_PHASE_PROF build)")
     args = ap.parse_args()
     from workload_files import make_c4, make_c5
     from file_streams import stripe_streams
@@ -50,7 +53,7 @@ def main():
     variants = [int(x) for x in args.variants.split(",")]
     factors = [int(x) for x in args.factors.split(",")]
     for col, kind, data in streams:
-        if kind not in ("PRESENT", "DATA", "LENGTH") or data.size < args.min_bytes:
+        if kind not in args.kinds.split(",") or data.size < args.min_bytes:
             continue
         ek = enc[col][0] if col < len(enc) else 0
         byte_rle = kind == "PRESENT"
@@ -104,12 +107,27 @@ def main():
                     e1.synchronize()
                     ts.append(e0.elapsed_time(e1) / args.iters)
                 ms = float(np.median(ts))
+                phases = None
+                if args.phases and byte_rle:
+                    import ctypes
+                    f = L.orcg_debug_byterle_phases
+                    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+                    buf = (ctypes.c_ulonglong * 8)()
+                    f(buf, 8, 1)
+                    for _ in range(args.iters):
+                        run()
+                    ctx.synchronize()
+                    f(buf, 8, 1)
+                    # wall-clock ticks (100 MHz) summed over workgroups -> us per workgroup
+                    nwg = int(segs.shape[0]) * args.iters
+                    phases = [round(buf[k] * 0.01 / nwg, 3) for k in range(8)]
                 out_b = nvals * (1 if byte_rle else 8)
                 print(json.dumps({"col": col, "kind": kind, "enc": ek, "bytes": int(data.size), "values": int(nvals),
                                   "B_per_value": round(data.size / max(nvals, 1), 3),
                                   "segments": int(segs.shape[0]), "variant": var, "ms": round(ms, 4),
                                   "Gvalues_s": round(nvals / ms / 1e6, 1),
-                                  "GBps": round((data.size + out_b) / ms / 1e6, 1)}), flush=True)
+                                  "GBps": round((data.size + out_b) / ms / 1e6, 1), "phases_us_per_wg": phases}),
+                      flush=True)
         ctx.set_rlev2_variant(0)
 
 

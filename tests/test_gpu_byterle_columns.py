@@ -208,3 +208,61 @@ def test_integer_column_with_present(orc):
     np.testing.assert_array_equal(gnn, onn)
     np.testing.assert_array_equal(got[gnn == 1], ovals[onn == 1])
     assert np.all(got[gnn == 0] == 0)  # untouched (zero-initialised) slots
+
+
+def _present_like(rng, nrows, null_frac):
+    """PRESENT-shaped bits (the reference writer's byte RLE of them): random
+    nulls at `null_frac`, so most groups are short runs of 0xFF and short
+    literals (~4-5 stream bytes per group at 10 %)."""
+    bits = (rng.random(nrows) >= null_frac).astype(np.uint8)
+    return bits, np.packbits(bits).tobytes()
+
+
+@pytest.mark.parametrize("null_frac", [0.0, 0.01, 0.1, 0.5, 0.97])
+@pytest.mark.parametrize("seg_bytes", [300, 4096, 20000, 1 << 30])
+def test_boolean_segments_of_every_size(orc, null_frac, seg_bytes):
+    """The parallel group discovery over windows of every fill (segments
+    shorter than a window, several windows per segment, one segment for the
+    whole stream) on PRESENT-shaped data, plus the set-row count the file
+    reader takes its non-null counts from."""
+    import ctypes
+
+    import torch
+
+    rng = np.random.default_rng(int(null_frac * 100) + seg_bytes % 97)
+    bits, raw = _present_like(rng, 400_003, null_frac)
+    enc = byte_rle_encode(raw, rng)
+    plan = orc.BytePlan(enc, max_segment_bytes=seg_bytes, max_segment_values=1 << 40)
+    segs = torch.from_numpy(plan.segments().view(np.int64)).cuda()
+    src = torch.from_numpy(np.frombuffer(enc, dtype=np.uint8).copy()).cuda()
+    ctx = orc.default_context(0)
+    full = np.unpackbits(np.frombuffer(raw, dtype=np.uint8))
+    n = bits.size
+    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    orc.byterle_decode_device(ctx, src, segs, n, out, boolean=True)
+    ctx.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), full[:n])
+    # decoded bytes (non-boolean) at an offset range
+    outb = torch.zeros(len(raw) - 5, dtype=torch.uint8, device="cuda")
+    orc.byterle_decode_device(ctx, src, segs, len(raw) - 5, outb, value_begin=5)
+    ctx.synchronize()
+    np.testing.assert_array_equal(outb.cpu().numpy(), np.frombuffer(raw, dtype=np.uint8)[5:])
+    del ctypes
+
+
+def test_truncated_stream_reports_first_bad_group(orc):
+    """A stream cut inside a literal group: the reference's "bad read in
+    nextBuffer" is raised for the first value of that group, whichever
+    thread of the window finds it."""
+    rng = np.random.default_rng(3)
+    raw = random_bytes(rng, 30_000)
+    enc = byte_rle_encode(raw, rng)
+    for cut in (len(enc) - 1, len(enc) // 2 + 7, 4097, 130):
+        bad = enc[:cut]
+        od = oracle.ByteRleDecoder(bad, boolean=False)
+        gd = orc.ByteRleDecoder(bad, boolean=False)
+        with pytest.raises(Exception) as we:
+            od.next(len(raw))
+        with pytest.raises(orc.ParseError) as ge:
+            gd.next(len(raw))
+        assert "bad read in nextBuffer" in str(ge.value) and str(we.value) in str(ge.value)
