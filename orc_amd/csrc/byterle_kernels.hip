@@ -11,8 +11,8 @@
 // its first decoded byte). The segment streams through an LDS window (4 KB of
 // group starts + the longest group's tail, one coalesced 16-B load per
 // thread); the window's group starts are found in parallel (chunk exits,
-// block hops, a workgroup scan: byterle_kernel below), short groups are
-// expanded by the thread that found them and long ones by a whole wave.
+// block hops, a workgroup scan: byterle_kernel below) and the decoded bytes
+// pass through an LDS stage to coalesced stores.
 // In boolean mode every decoded byte becomes 8 output rows (chars 0/1).
 #include "rlev2_device.hh"
 
@@ -75,8 +75,6 @@ constexpr uint32_t kBChunk = 4096;                 // groups starting in a windo
 constexpr uint32_t kBWinBytes = kBChunk + 256;     // + the longest group's tail (129 B) + the 16-B alignment
 constexpr uint32_t kBBlock = 128;                  // hop granularity of the chain walk
 constexpr uint32_t kBBlocks = kBChunk / kBBlock;
-constexpr uint32_t kBShort = 32;                   // groups decoding to fewer bytes: expanded by their thread
-constexpr uint32_t kBMaxLong = kBChunk / 2;        // every group is >= 2 bytes
 constexpr uint16_t kBNone = 0xffffu;
 
 typedef uint32_t bu4 __attribute__((ext_vector_type(4)));
@@ -111,8 +109,9 @@ __device__ __forceinline__ uint32_t group_dec(uint32_t h) { return h < 0x80 ? h 
 //   4. each thread hops from its block's first start to its own chunk
 //      (<= 7 hops) and walks the groups starting in its chunk (<= 8);
 //   5. a workgroup scan of the groups' decoded bytes gives each group its
-//      first decoded index; short groups are expanded by their thread, long
-//      ones (runs of up to 130 copies, full literals) by a whole wave.
+//      first decoded index;
+//   6. the groups' decoded bytes go through an LDS stage (16 KB at a time)
+//      and leave it with coalesced stores.
 // Errors are reported per group with atomicMin on (decoded index, code), so
 // the earliest in stream order wins, as the reference's serial loop raises
 // it (ByteRleDecoderImpl::nextInternal, :449-505).
@@ -126,14 +125,12 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
   uint64_t prof_last_ = wall_clock64();
 #endif
   __shared__ __attribute__((aligned(16))) uint32_t s_win[(kBWinBytes + 256) / 4];
-  // s_exit / s_exit2 (steps 1-4), then the long-group list (step 5)
+  // s_exit / s_exit2 (steps 1-4), then the stage of decoded bytes (step 6)
   __shared__ __attribute__((aligned(16))) uint16_t s_exit[2 * kBChunk];
   __shared__ uint16_t s_bentry[kBBlocks + 1];
   __shared__ uint32_t s_wsum[2][kBThreads / kWave];
-  __shared__ uint32_t s_ctl[4];  // next window position, long groups, error seen
+  __shared__ uint32_t s_ctl[4];  // next window position, -, error seen
   uint16_t* s_exit2 = s_exit + kBChunk;
-  uint16_t* s_long_off = s_exit;                       // aliases s_exit (dead by step 5)
-  uint32_t* s_long_dec = (uint32_t*)(s_exit + kBMaxLong);  // 2 * kBMaxLong u16 = kBMaxLong u32
   const uint8_t* s_bytes = (const uint8_t*)s_win;
   const uint64_t g = blockIdx.x;
   const int tid = (int)threadIdx.x;
@@ -264,6 +261,10 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
       dec_total += d;
     }
     const uint32_t np = s_ctl[0];
+    // 5b. my groups in stream order: the errors (the serial loop's checks, at
+    // each group's decoded index; atomicMin keeps the earliest) and how many
+    // of them are decoded (none past an error or past the bytes needed)
+    uint32_t nvalid = 0;
     if (qs != kBNone) {
       uint32_t p = qs, d = dec_base;
       while (p < cs + 16 && p < lim) {
@@ -276,14 +277,7 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
           s_ctl[2] = 1;
           break;
         }
-        if (L < kBShort) {
-          const uint32_t rb = s_bytes[p + 1];
-          for (uint32_t j = 0; j < L; ++j) emit<kBool>(dst, di + j, h < 0x80 ? rb : s_bytes[p + 1 + j], begin, end, ones);
-        } else {
-          const uint32_t k = atomicAdd(&s_ctl[1], 1u);
-          s_long_off[k] = (uint16_t)p;
-          s_long_dec[k] = d;
-        }
+        ++nvalid;
         if ((uint64_t)p + gl > seg_left) {  // the group runs past the segment
           report(err, di + L, kErrBadSegment);
           s_ctl[2] = 1;
@@ -293,20 +287,39 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
         d += L;
       }
     }
-    __syncthreads();
-    BPROF_MARK(5);
-    // long groups: one wave per group, one decoded byte per lane
-    const uint32_t nlong = s_ctl[1];
-    for (uint32_t k = (uint32_t)wave; k < nlong; k += kBThreads / kWave) {
-      const uint32_t o = s_long_off[k];
-      const uint32_t d0 = s_long_dec[k];
-      const uint32_t h = s_bytes[o];
-      const uint32_t rb = s_bytes[o + 1];
-      const uint32_t len = group_dec(h);
-      for (uint32_t j = (uint32_t)lane; j < len; j += kWave) {
-        const uint32_t b = h < 0x80 ? rb : s_bytes[o + 1u + j];
-        emit<kBool>(dst, vi + d0 + j, b, begin, end, ones);
+    // 6. expansion through an LDS stage of decoded bytes (s_exit's 16 KB,
+    // dead now), one stage-full at a time: each thread copies its groups'
+    // bytes in (runs as word fills), then the workgroup writes the stage out
+    // with consecutive lanes on consecutive output (coalesced stores; a
+    // thread storing its own groups scatters every store over 64 lines)
+    uint8_t* s_stage = (uint8_t*)s_exit;
+    constexpr uint32_t kStage = 2 * kBChunk * sizeof(uint16_t);
+    for (uint32_t sb = 0; sb < dec_total; sb += kStage) {
+      uint32_t p = qs, d = dec_base;
+      for (uint32_t k = 0; k < nvalid && d < sb + kStage; ++k) {
+        const uint32_t h = chunk_byte(mine, p - cs);
+        const uint32_t L = group_dec(h);
+        const uint32_t a = d > sb ? d : sb, b = d + L < sb + kStage ? d + L : sb + kStage;
+        if (a < b) {
+          uint32_t x = a - sb;
+          const uint32_t xe = b - sb;
+          if (h < 0x80) {
+            const uint32_t v = s_bytes[p + 1];
+            for (; x < xe && (x & 3u); ++x) s_stage[x] = (uint8_t)v;
+            for (; x + 4 <= xe; x += 4) *(uint32_t*)(s_stage + x) = v * 0x01010101u;
+            for (; x < xe; ++x) s_stage[x] = (uint8_t)v;
+          } else {
+            const uint8_t* lit = s_bytes + p + 1 + (a - d);
+            for (uint32_t y = 0; x < xe; ++x, ++y) s_stage[x] = lit[y];
+          }
+        }
+        p += group_len(h);
+        d += L;
       }
+      __syncthreads();
+      const uint32_t n = dec_total - sb < kStage ? dec_total - sb : kStage;
+      for (uint32_t k = (uint32_t)tid; k < n; k += kBThreads) emit<kBool>(dst, vi + sb + k, s_stage[k], begin, end, ones);
+      __syncthreads();
     }
     const bool stop = s_ctl[2] != 0;
     __syncthreads();  // the window and the tables are rewritten by the next pass

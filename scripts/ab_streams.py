@@ -57,10 +57,12 @@ def main():
             continue
         ek = enc[col][0] if col < len(enc) else 0
         byte_rle = kind == "PRESENT"
-        if kind == "DATA" and ek not in (1, 3):  # DIRECT_V2 / DICTIONARY_V2 integer-coded DATA only
+        if not byte_rle and ek not in (2, 3):  # RLEv2 streams only (DIRECT_V2 / DICTIONARY_V2 columns)
             continue
-        # DATA of an int column is signed; dictionary indices and lengths are not
-        signed = kind == "DATA" and ek == 1
+        if kind == "DATA" and ek == 2 and data.size > 8 * 10_000_000:
+            continue
+        # DATA of a DIRECT_V2 int column is signed; dictionary indices and lengths are not
+        signed = kind == "DATA" and ek == 2
         with torch.cuda.stream(stream):
             d_src = torch.from_numpy(data).cuda()
         ref = None
@@ -108,6 +110,22 @@ def main():
                     ts.append(e0.elapsed_time(e1) / args.iters)
                 ms = float(np.median(ts))
                 phases = None
+                if args.phases and not byte_rle:
+                    import ctypes
+                    f = L.orcg_debug_phase_counters
+                    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+                    buf = (ctypes.c_ulonglong * 16)()
+                    f(buf, 16, 1)
+                    for _ in range(args.iters):
+                        run()
+                    ctx.synchronize()
+                    f(buf, 16, 1)
+                    nwg = int(segs.shape[0]) * args.iters
+                    names = ["fill", "serial_walk", "serial_expand", "dense_dp", "dense_chain", "dense_emit",
+                             "dense_expand"]
+                    phases = {nm: round(buf[k] * 0.01 / nwg, 3) for k, nm in enumerate(names)}
+                    phases["runs_walked_per_wg"] = round(buf[8] / nwg, 1)
+                    phases["serial_passes_per_wg"] = round(buf[9] / nwg, 2)
                 if args.phases and byte_rle:
                     import ctypes
                     f = L.orcg_debug_byterle_phases

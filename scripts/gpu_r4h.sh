@@ -1,0 +1,20 @@
+#!/bin/bash
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out; mkdir -p $OUT
+: > $OUT/status.log
+run() {
+  local name=$1 t=$2; shift 2
+  echo "[$(date +%T)] start $name" >> $OUT/status.log
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >> $OUT/status.log
+  case $rc in 124|137|134|139) echo "fatal rc=$rc in $name, stopping" >> $OUT/status.log; exit $rc;; esac
+  return $rc
+}
+export TMPDIR=/tmp
+run t_split 300 env ORCG_SPLIT=8 python -u -m pytest tests/test_gpu_rlev2.py -k split -m gpu -x -q --timeout 120 --timeout-method thread
+run ph_c5 300 env ORCG_LIB=liborcgpu_prof.so python scripts/ab_streams.py --workload c5 --rows 2600000 --factors 1 --phases --kinds DATA,LENGTH --variants 0,2,6
+run ph_c4 300 env ORCG_LIB=liborcgpu_prof.so python scripts/ab_streams.py --workload c4 --rows 1860000 --factors 1 --phases --kinds DATA,LENGTH --variants 0,6
+run ph_c5_s4 300 env ORCG_SPLIT=4 ORCG_LIB=liborcgpu_prof.so python scripts/ab_streams.py --workload c5 --rows 2600000 --factors 1 --phases --kinds DATA --variants 2,6
+echo done >> $OUT/status.log

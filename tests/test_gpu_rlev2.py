@@ -414,3 +414,40 @@ def test_queued_segment_reports_truncation():
             orc_amd.rlev2_decode(bad, v.size + 1, True)
         assert str(got.value) == str(want.value), variant
     ctx.set_rlev2_variant(0)
+
+
+@pytest.mark.parametrize("kind", ["repeat", "delta", "patched", "wide"])
+def test_split_launches_every_variant(kind):
+    """Few large segments (a file's child-column row groups), every pinned
+    instance, full range and value windows whose ends fall inside runs,
+    against the generated values (the encoder's input, checked against the
+    oracle below). With ORCG_SPLIT=k (k > 1) in the environment the launches
+    split each segment's values over k workgroups (rlev2_tiled.hip
+    auto_split), each one walking the runs before its share: the same test
+    covers that path."""
+    import torch
+
+    import orc_amd as orc
+    from oracle import oracle
+
+    rng = np.random.default_rng(11)
+    v, data, _ = _stream_with_positions(orc, rng, kind, 600_000, 10_000)
+    n = v.size
+    assert np.array_equal(oracle.rlev2_decode(data.tobytes(), n, True), v)
+    ctx = orc.default_context(0)
+    d_src = torch.from_numpy(data).cuda()
+    for seg_values in (40_000, 150_000):  # 15 / 4 segments: split 8 / 8
+        plan = orc.Plan(data, 1 << 30, seg_values)
+        segs = torch.from_numpy(plan.segments().view(np.int64)).cuda()
+        try:
+            for variant in orc.rlev2_variants():
+                ctx.set_rlev2_variant(variant)
+                for a, b in [(0, n), (1, n - 1), (12_345, 333_333), (n - 513, n)]:
+                    out = torch.zeros(b - a, dtype=torch.int64, device="cuda")
+                    orc.decode_device(ctx, d_src, segs, b - a, True, out, value_begin=a)
+                    ctx.synchronize()
+                    got = out.cpu().numpy()
+                    assert np.array_equal(got, v[a:b]), "variant %d segs %d range %d-%d: first mismatch at %d" % (
+                        variant, segs.shape[0], a, b, a + int(np.argmax(got != v[a:b])))
+        finally:
+            ctx.set_rlev2_variant(0)
