@@ -406,13 +406,14 @@ def run_file_workload(args, dist, world, rank, device):
         import pyarrow.orc as po
 
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from file_parity import first_difference
+        from arrow_parity import first_difference_arrow
 
-        got = r.read_stripe(first).to_pylist()
-        diff = first_difference(po.ORCFile(path).read_stripe(first).to_pylist(), got)
-        if diff:
-            raise SystemExit("%s stripe %d mismatch against pyarrow on rank %d: %s" % (args.workload, first, rank, diff))
-        check = "stripe %d (%d rows) equal to pyarrow on every rank" % (first, len(got))
+        pf = po.ORCFile(path)
+        for s in range(first, last):
+            diff = first_difference_arrow(pf.read_stripe(s), r.read_stripe(s), r)
+            if diff:
+                raise SystemExit("%s stripe %d mismatch against pyarrow on rank %d: %s" % (args.workload, s, rank, diff))
+        check = "every stripe of every rank equal to pyarrow (value buffers, tests/arrow_parity.py)"
     if rank == 0:
         step_s = elapsed / args.steps
         dev = dev_s / args.steps

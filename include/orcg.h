@@ -48,6 +48,13 @@ typedef struct orcg_ctx orcg_ctx;
  * MemoryPool.hh:27-33) plays for host buffers. */
 int orcg_ctx_create(int device, orcg_ctx** out);
 void orcg_ctx_destroy(orcg_ctx* ctx);
+
+/* Pinned (page-locked) host memory, the allocator of the C++ adapter's
+ * PinnedMemoryPool (an orc::MemoryPool, c++/include/orc/MemoryPool.hh:27-33):
+ * batches in pinned memory can be DMA'd to a device without a staging copy.
+ * NULL on failure. */
+void* orcg_host_alloc(uint64_t bytes);
+void orcg_host_free(void* p);
 /* Use an external stream (e.g. torch.cuda.current_stream().cuda_stream);
  * NULL restores the context's own stream.
  * Ordering contract of every *_device entry: the launch is queued on the

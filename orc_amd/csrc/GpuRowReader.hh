@@ -22,22 +22,32 @@
 //
 // next() follows RowReaderImpl::next (c++/src/Reader.cc:1392-1442): at most
 // capacity rows, never across a stripe. The GPU decodes a whole stripe into
-// HBM once (host decompression, one H2D, HIP kernels); each batch copies its
-// row range of every selected column into the batch's host buffers. String
-// data pointers point into the batch's host copy of the string bytes (the
-// dictionary, or the span of direct strings the batch covers). Inside the
-// reference build these stand-in batch classes are the orc::*VectorBatch
-// classes themselves (same member names).
+// HBM once (host decompression, one H2D, HIP kernels) and the row reader's
+// worker copies it into a pinned host slab; each batch copies its row range of
+// every selected column into the batch's buffers, DataBuffers allocated from
+// the caller's MemoryPool (ReaderOptions::setMemoryPool, Reader.hh:123, 163;
+// MemoryPool.hh:27-33; PinnedMemoryPool for batches that go to a device
+// next). The copies of one batch run on the caller's thread and a few helper
+// threads of the row reader (CopyPool). String data pointers point into the
+// batch's host copy of the string bytes (the dictionary, or the span of direct
+// strings the batch covers). Inside the reference build these stand-in batch
+// classes are the orc::*VectorBatch classes themselves (same member names).
 #pragma once
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <functional>
 #include <list>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/orcg_reader.h"
@@ -46,58 +56,274 @@
 namespace orcg {
 namespace cxx {
 
+// orc::MemoryPool (c++/include/orc/MemoryPool.hh:27-33): the caller's
+// allocator for batch memory.
+class MemoryPool {
+ public:
+  virtual ~MemoryPool() = default;
+  virtual char* malloc(uint64_t size) = 0;
+  virtual void free(char* p) = 0;
+};
+class DefaultMemoryPool : public MemoryPool {
+ public:
+  char* malloc(uint64_t size) override { return static_cast<char*>(std::malloc(size ? size : 1)); }
+  void free(char* p) override { std::free(p); }
+};
+// orc::getDefaultPool (MemoryPool.cc)
+inline MemoryPool* getDefaultPool() {
+  static DefaultMemoryPool pool;
+  return &pool;
+}
+// Pinned host memory (orcg_host_alloc): batches a caller DMAs to a device.
+class PinnedMemoryPool : public MemoryPool {
+ public:
+  char* malloc(uint64_t size) override {
+    char* p = static_cast<char*>(orcg_host_alloc(size));
+    if (!p) throw std::bad_alloc();
+    return p;
+  }
+  void free(char* p) override { orcg_host_free(p); }
+};
+
+// orc::DataBuffer<T> (c++/include/orc/MemoryPool.hh:35-80) for trivially
+// copyable T: memory from the pool; resize keeps the contents and leaves new
+// elements uninitialised, as the reference's does for POD types.
+template <typename T>
+class DataBuffer {
+  static_assert(std::is_trivially_copyable<T>::value, "DataBuffer holds trivially copyable values");
+
+ public:
+  explicit DataBuffer(MemoryPool& pool = *getDefaultPool(), uint64_t size = 0) : pool_(&pool) { resize(size); }
+  ~DataBuffer() {
+    if (buf_) pool_->free(reinterpret_cast<char*>(buf_));
+  }
+  DataBuffer(const DataBuffer&) = delete;
+  DataBuffer& operator=(const DataBuffer&) = delete;
+  DataBuffer(DataBuffer&& o) noexcept : pool_(o.pool_), buf_(o.buf_), size_(o.size_), cap_(o.cap_) {
+    o.buf_ = nullptr;
+    o.size_ = o.cap_ = 0;
+  }
+  T* data() { return buf_; }
+  const T* data() const { return buf_; }
+  uint64_t size() const { return size_; }
+  uint64_t capacity() const { return cap_; }
+  bool empty() const { return size_ == 0; }
+  T& operator[](uint64_t i) { return buf_[i]; }
+  const T& operator[](uint64_t i) const { return buf_[i]; }
+  T* begin() { return buf_; }
+  T* end() { return buf_ + size_; }
+  const T* begin() const { return buf_; }
+  const T* end() const { return buf_ + size_; }
+  MemoryPool& getMemoryPool() const { return *pool_; }
+  void reserve(uint64_t n) {
+    if (n <= cap_) return;
+    T* nb = reinterpret_cast<T*>(pool_->malloc(n * sizeof(T)));
+    if (size_) memcpy(nb, buf_, size_ * sizeof(T));
+    if (buf_) pool_->free(reinterpret_cast<char*>(buf_));
+    buf_ = nb;
+    cap_ = n;
+  }
+  void resize(uint64_t n) {
+    if (n > cap_) reserve(std::max<uint64_t>(n, cap_ + cap_ / 2));
+    size_ = n;
+  }
+  void assign(uint64_t n, const T& v) {
+    resize(n);
+    for (uint64_t i = 0; i < n; ++i) buf_[i] = v;
+  }
+  void zeroOut() {
+    if (size_) memset(buf_, 0, size_ * sizeof(T));
+  }
+
+ private:
+  MemoryPool* pool_;
+  T* buf_ = nullptr;
+  uint64_t size_ = 0, cap_ = 0;
+};
+
+// The copies of one batch, spread over the calling thread and a few helper
+// threads that spin between batches (a batch of 1,024 rows is ~10-30 us of
+// copying; waking sleeping threads per batch would cost more than it saves)
+// and sleep after ~50 us without work.
+class CopyPool {
+ public:
+  struct Task {
+    void* dst;
+    const void* src;
+    uint64_t bytes;
+  };
+  explicit CopyPool(unsigned helpers) {
+    for (unsigned i = 0; i < helpers; ++i) ts_.emplace_back([this] { loop(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+      stop_flag_.store(true, std::memory_order_relaxed);
+    }
+    cv_.notify_all();
+    for (auto& t : ts_) t.join();
+  }
+  CopyPool(const CopyPool&) = delete;
+  CopyPool& operator=(const CopyPool&) = delete;
+  // run every copy of `tasks` (cut into <= 64 KB pieces) and return when all are done
+  void run(const std::vector<Task>& tasks) {
+    uint64_t total = 0;
+    for (const Task& t : tasks) total += t.bytes;
+    if (ts_.empty() || total < (96u << 10)) {
+      for (const Task& t : tasks)
+        if (t.bytes) memcpy(t.dst, t.src, t.bytes);
+      return;
+    }
+    work_.clear();
+    constexpr uint64_t kPiece = 64u << 10;
+    for (const Task& t : tasks)
+      for (uint64_t o = 0; o < t.bytes; o += kPiece)
+        work_.push_back(Task{(char*)t.dst + o, (const char*)t.src + o, std::min(kPiece, t.bytes - o)});
+    const uint64_t n = work_.size();
+    if (n >= 0xffff) {  // (the claim word holds 16 bits of task count)
+      for (const Task& t : work_) memcpy(t.dst, t.src, t.bytes);
+      return;
+    }
+    const uint64_t g = ++gen_;
+    done_.store(0, std::memory_order_relaxed);
+    // (generation, task count, next index): a helper that claims an index
+    // of a finished generation sees it and takes nothing
+    claim_.store((g << 48) | (n << 32), std::memory_order_release);
+    if (sleepers_.load(std::memory_order_acquire)) {
+      std::lock_guard<std::mutex> lk(m_);
+      cv_.notify_all();
+    }
+    help(g);
+    while (done_.load(std::memory_order_acquire) < n) {
+    }
+  }
+
+ private:
+  void help(uint64_t g) {
+    // claims by compare-and-swap: a thread still on an older generation
+    // must not consume an index of the current one
+    uint64_t c = claim_.load(std::memory_order_acquire);
+    for (;;) {
+      const uint64_t cg = c >> 48, cn = (c >> 32) & 0xffff, k = c & 0xffffffffu;
+      if (cg != (g & 0xffff) || k >= cn) return;
+      if (!claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+      const Task& t = work_[k];
+      memcpy(t.dst, t.src, t.bytes);
+      done_.fetch_add(1, std::memory_order_acq_rel);
+      c = claim_.load(std::memory_order_acquire);
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      uint64_t c = 0;
+      bool got = false;
+      for (int spin = 0; spin < 20000; ++spin) {
+        c = claim_.load(std::memory_order_acquire);
+        if ((c >> 48) != (seen & 0xffff) && (c & 0xffffffffu) < ((c >> 32) & 0xffff)) {
+          got = true;
+          break;
+        }
+        if (stop_flag_.load(std::memory_order_relaxed)) return;
+      }
+      if (!got) {
+        std::unique_lock<std::mutex> lk(m_);
+        sleepers_.fetch_add(1, std::memory_order_acq_rel);
+        cv_.wait(lk, [&] {
+          const uint64_t x = claim_.load(std::memory_order_acquire);
+          return stop_ || ((x >> 48) != (seen & 0xffff) && (x & 0xffffffffu) < ((x >> 32) & 0xffff));
+        });
+        sleepers_.fetch_sub(1, std::memory_order_acq_rel);
+        if (stop_) return;
+        c = claim_.load(std::memory_order_acquire);
+      }
+      seen = c >> 48;
+      help(seen);
+    }
+  }
+  std::vector<std::thread> ts_;
+  std::vector<Task> work_;
+  uint64_t gen_ = 0;
+  std::atomic<uint64_t> claim_{0};
+  std::atomic<uint64_t> done_{0};
+  std::atomic<int> sleepers_{0};
+  std::atomic<bool> stop_flag_{false};
+  std::mutex m_;
+  std::condition_variable cv_;
+  bool stop_ = false;
+};
+
 struct Int128 {  // orc::Int128 member order (c++/include/orc/Int128.hh:325-326)
   int64_t highbits = 0;
   uint64_t lowbits = 0;
 };
 
+// which concrete batch a ColumnVectorBatch is (fill() switches on it instead
+// of trying dynamic_casts)
+enum class BatchClass {
+  kLong, kInt, kShort, kByte, kDouble, kFloat, kString, kEncodedString, kDecimal64, kDecimal128, kTimestamp,
+  kList, kMap, kStruct, kUnion
+};
+
 struct ColumnVectorBatch {
-  ColumnVectorBatch(uint32_t kind_, uint64_t cap) : kind(kind_), capacity(cap) {}
+  ColumnVectorBatch(uint32_t kind_, uint64_t cap, MemoryPool& pool, BatchClass cls_)
+      : kind(kind_), capacity(cap), notNull(pool, cap), memoryPool(pool), cls(cls_) {}
   virtual ~ColumnVectorBatch() = default;
   uint32_t kind;  // orc::TypeKind
   uint64_t capacity;
   uint64_t numElements = 0;
-  std::vector<char> notNull;
+  DataBuffer<char> notNull;  // valid when hasNulls (ColumnReader::next leaves it alone otherwise)
   bool hasNulls = false;
   bool isEncoded = false;
+  MemoryPool& memoryPool;
+  const BatchClass cls;
 };
+#define ORCG_BATCH(Name, Cls)                                              \
+  Name(uint32_t k, uint64_t cap, MemoryPool& pool = *getDefaultPool())     \
+      : ColumnVectorBatch(k, cap, pool, BatchClass::Cls)
 struct LongVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<int64_t> data;
+  ORCG_BATCH(LongVectorBatch, kLong), data(pool, cap) {}
+  DataBuffer<int64_t> data;
 };
 // RowReaderOptions::setUseTightNumericVector batches (Vector.hh IntegerVectorBatch<T>,
 // FloatingVectorBatch<float>): BOOLEAN / BYTE -> Byte, SHORT -> Short, INT ->
 // Int, FLOAT -> Float (ColumnReader.cc:1703-1790)
 struct IntVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<int32_t> data;
+  ORCG_BATCH(IntVectorBatch, kInt), data(pool, cap) {}
+  DataBuffer<int32_t> data;
 };
 struct ShortVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<int16_t> data;
+  ORCG_BATCH(ShortVectorBatch, kShort), data(pool, cap) {}
+  DataBuffer<int16_t> data;
 };
 struct ByteVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<int8_t> data;
+  ORCG_BATCH(ByteVectorBatch, kByte), data(pool, cap) {}
+  DataBuffer<int8_t> data;
 };
 struct DoubleVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<double> data;
+  ORCG_BATCH(DoubleVectorBatch, kDouble), data(pool, cap) {}
+  DataBuffer<double> data;
 };
 struct FloatVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<float> data;
+  ORCG_BATCH(FloatVectorBatch, kFloat), data(pool, cap) {}
+  DataBuffer<float> data;
 };
 struct StringVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<char*> data;
-  std::vector<int64_t> length;
-  std::vector<char> blob;  // host copy of the string bytes the batch points into
+  ORCG_BATCH(StringVectorBatch, kString), data(pool, cap), length(pool, cap), blob(pool) {}
+  DataBuffer<char*> data;
+  DataBuffer<int64_t> length;
+  DataBuffer<char> blob;  // host copy of the string bytes the batch points into
+
+ protected:
+  StringVectorBatch(uint32_t k, uint64_t cap, MemoryPool& pool, BatchClass c)
+      : ColumnVectorBatch(k, cap, pool, c), data(pool, cap), length(pool, cap), blob(pool) {}
 };
 // orc::StringDictionary (Vector.hh:232-254)
 struct StringDictionary {
-  std::vector<char> dictionaryBlob;
-  std::vector<int64_t> dictionaryOffset;
+  explicit StringDictionary(MemoryPool& pool = *getDefaultPool()) : dictionaryBlob(pool), dictionaryOffset(pool) {}
+  DataBuffer<char> dictionaryBlob;
+  DataBuffer<int64_t> dictionaryOffset;
   void getValueByIndex(int64_t index, char*& valPtr, int64_t& length) {
     if (index < 0 || static_cast<uint64_t>(index) + 1 >= dictionaryOffset.size())
       throw std::out_of_range("index out of range.");
@@ -108,44 +334,46 @@ struct StringDictionary {
 // orc::EncodedStringVectorBatch (Vector.hh:256-269): with lazy decoding the
 // dictionary columns fill index + dictionary only
 struct EncodedStringVectorBatch : StringVectorBatch {
-  using StringVectorBatch::StringVectorBatch;
+  EncodedStringVectorBatch(uint32_t k, uint64_t cap, MemoryPool& pool = *getDefaultPool())
+      : StringVectorBatch(k, cap, pool, BatchClass::kEncodedString), index(pool, cap) {}
   std::shared_ptr<StringDictionary> dictionary;
-  std::vector<int64_t> index;
+  DataBuffer<int64_t> index;
 };
 struct Decimal64VectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
+  ORCG_BATCH(Decimal64VectorBatch, kDecimal64), values(pool, cap) {}
   int32_t precision = 0, scale = 0;
-  std::vector<int64_t> values;
+  DataBuffer<int64_t> values;
 };
 struct Decimal128VectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
+  ORCG_BATCH(Decimal128VectorBatch, kDecimal128), values(pool, cap) {}
   int32_t precision = 0, scale = 0;
-  std::vector<Int128> values;
+  DataBuffer<Int128> values;
 };
 struct TimestampVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<int64_t> data, nanoseconds;
+  ORCG_BATCH(TimestampVectorBatch, kTimestamp), data(pool, cap), nanoseconds(pool, cap) {}
+  DataBuffer<int64_t> data, nanoseconds;
 };
 struct ListVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<int64_t> offsets;
+  ORCG_BATCH(ListVectorBatch, kList), offsets(pool, cap + 1) {}
+  DataBuffer<int64_t> offsets;
   std::unique_ptr<ColumnVectorBatch> elements;
 };
 struct MapVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<int64_t> offsets;
+  ORCG_BATCH(MapVectorBatch, kMap), offsets(pool, cap + 1) {}
+  DataBuffer<int64_t> offsets;
   std::unique_ptr<ColumnVectorBatch> keys, elements;
 };
 struct StructVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
+  ORCG_BATCH(StructVectorBatch, kStruct) {}
   std::vector<std::unique_ptr<ColumnVectorBatch>> fields;
 };
 struct UnionVectorBatch : ColumnVectorBatch {
-  using ColumnVectorBatch::ColumnVectorBatch;
-  std::vector<unsigned char> tags;
-  std::vector<uint64_t> offsets;
+  ORCG_BATCH(UnionVectorBatch, kUnion), tags(pool, cap), offsets(pool, cap) {}
+  DataBuffer<unsigned char> tags;
+  DataBuffer<uint64_t> offsets;
   std::vector<std::unique_ptr<ColumnVectorBatch>> children;
 };
+#undef ORCG_BATCH
 
 // orc::RowReaderOptions (the options the decode path honours)
 class RowReaderOptions {
@@ -183,6 +411,20 @@ class RowReaderOptions {
   bool tight_ = false;
 };
 
+// orc::ReaderOptions (c++/include/orc/Reader.hh:112-200): the memory pool
+// batches and dictionaries are allocated from.
+class ReaderOptions {
+ public:
+  ReaderOptions& setMemoryPool(MemoryPool& pool) {
+    pool_ = &pool;
+    return *this;
+  }
+  MemoryPool* getMemoryPool() const { return pool_; }
+
+ private:
+  MemoryPool* pool_ = getDefaultPool();
+};
+
 class Reader;
 
 class RowReader {
@@ -209,17 +451,29 @@ class RowReader {
   // as the reference's batches point into the column reader's dictionary)
   uint64_t dict_stripe_ = ~0ull;
   std::map<uint32_t, std::shared_ptr<StringDictionary>> dicts_;
-  std::map<uint32_t, std::shared_ptr<std::vector<char>>> blobs_;
-  // per type: the children fill() visits (struct: the selected fields)
+  std::map<uint32_t, std::shared_ptr<DataBuffer<char>>> blobs_;
+  // per type: the children fill() visits (struct: the selected fields) and
+  // the type's scale / precision (decimals)
   std::vector<std::vector<uint32_t>> subs_;
   std::vector<uint8_t> subs_known_;
+  std::vector<orcg_type_info> types_;
   const std::vector<uint32_t>& subs(uint32_t id, uint32_t kind);
   void new_stripe();
+  // the batch's bulk copies (slab -> batch buffers), run together at the end
+  // of next() on this thread and the copy pool's helpers
+  std::vector<CopyPool::Task> copies_;
+  std::unique_ptr<CopyPool> pool_;
+  template <typename T>
+  void copy(DataBuffer<T>& dst, const void* src, uint64_t count, uint64_t first = 0) {
+    dst.resize(count);
+    if (count) copies_.push_back(CopyPool::Task{dst.data(), (const T*)src + first, count * sizeof(T)});
+  }
 };
 
 class Reader {
  public:
-  Reader(Context& ctx, const std::string& path) : ctx_(ctx) {
+  Reader(Context& ctx, const std::string& path, const ReaderOptions& opts = ReaderOptions())
+      : ctx_(ctx), pool_(opts.getMemoryPool()) {
     if (orcg_reader_open_file(ctx.get(), path.c_str(), &r_) != ORCG_OK) {
       const std::string m = orcg_reader_open_error();
       throw ParseError(m);
@@ -281,6 +535,7 @@ class Reader {
   std::unique_ptr<RowReader> createRowReader(const RowReaderOptions& opts) {
     return std::make_unique<RowReader>(*this, opts);
   }
+  MemoryPool& getMemoryPool() const { return *pool_; }
 
   // internals for RowReader
   void check(int rc) const {
@@ -290,20 +545,10 @@ class Reader {
     }
   }
   orcg_reader* get() const { return r_; }
-  template <typename T>
-  void copy(std::vector<T>& dst, const void* src, uint64_t count, uint64_t first = 0) {
-    dst.resize(count);
-    if (count) check(orcg_reader_copy_to_host(r_, dst.data(), (const T*)src + first, count * sizeof(T)));
-  }
-  // row reader views point into its pinned host slab: plain copies
-  template <typename T>
-  static void hcopy(std::vector<T>& dst, const void* src, uint64_t count, uint64_t first = 0) {
-    dst.resize(count);
-    if (count) memcpy(dst.data(), (const T*)src + first, count * sizeof(T));
-  }
 
  private:
   Context& ctx_;
+  MemoryPool* pool_;
   orcg_reader* r_ = nullptr;
 };
 
@@ -312,40 +557,41 @@ using Selected = std::function<bool(uint32_t)>;
 inline std::unique_ptr<ColumnVectorBatch> make_batch(const Reader& r, uint32_t id, uint64_t cap, bool lazy,
                                                      const Selected& sel, bool tight = false) {
   const orcg_type_info t = r.getType(id);
+  MemoryPool& pool = r.getMemoryPool();
   switch (t.kind) {
     case ORCG_TYPE_BOOLEAN:
     case ORCG_TYPE_BYTE:
-      if (tight) return std::make_unique<ByteVectorBatch>(t.kind, cap);
-      return std::make_unique<LongVectorBatch>(t.kind, cap);
+      if (tight) return std::make_unique<ByteVectorBatch>(t.kind, cap, pool);
+      return std::make_unique<LongVectorBatch>(t.kind, cap, pool);
     case ORCG_TYPE_SHORT:
-      if (tight) return std::make_unique<ShortVectorBatch>(t.kind, cap);
-      return std::make_unique<LongVectorBatch>(t.kind, cap);
+      if (tight) return std::make_unique<ShortVectorBatch>(t.kind, cap, pool);
+      return std::make_unique<LongVectorBatch>(t.kind, cap, pool);
     case ORCG_TYPE_INT:
-      if (tight) return std::make_unique<IntVectorBatch>(t.kind, cap);
-      return std::make_unique<LongVectorBatch>(t.kind, cap);
+      if (tight) return std::make_unique<IntVectorBatch>(t.kind, cap, pool);
+      return std::make_unique<LongVectorBatch>(t.kind, cap, pool);
     case ORCG_TYPE_FLOAT:
-      if (tight) return std::make_unique<FloatVectorBatch>(t.kind, cap);
-      return std::make_unique<DoubleVectorBatch>(t.kind, cap);
-    case ORCG_TYPE_DOUBLE: return std::make_unique<DoubleVectorBatch>(t.kind, cap);
+      if (tight) return std::make_unique<FloatVectorBatch>(t.kind, cap, pool);
+      return std::make_unique<DoubleVectorBatch>(t.kind, cap, pool);
+    case ORCG_TYPE_DOUBLE: return std::make_unique<DoubleVectorBatch>(t.kind, cap, pool);
     case ORCG_TYPE_STRING:
     case ORCG_TYPE_BINARY:
     case ORCG_TYPE_VARCHAR:
     case ORCG_TYPE_CHAR:
       // Type::createRowBatch: an encoded batch when lazy decoding is on
-      if (lazy) return std::make_unique<EncodedStringVectorBatch>(t.kind, cap);
-      return std::make_unique<StringVectorBatch>(t.kind, cap);
+      if (lazy) return std::make_unique<EncodedStringVectorBatch>(t.kind, cap, pool);
+      return std::make_unique<StringVectorBatch>(t.kind, cap, pool);
     case ORCG_TYPE_DECIMAL:
-      if (t.precision > 18 || t.precision == 0) return std::make_unique<Decimal128VectorBatch>(t.kind, cap);
-      return std::make_unique<Decimal64VectorBatch>(t.kind, cap);
+      if (t.precision > 18 || t.precision == 0) return std::make_unique<Decimal128VectorBatch>(t.kind, cap, pool);
+      return std::make_unique<Decimal64VectorBatch>(t.kind, cap, pool);
     case ORCG_TYPE_TIMESTAMP:
-    case ORCG_TYPE_TIMESTAMP_INSTANT: return std::make_unique<TimestampVectorBatch>(t.kind, cap);
+    case ORCG_TYPE_TIMESTAMP_INSTANT: return std::make_unique<TimestampVectorBatch>(t.kind, cap, pool);
     case ORCG_TYPE_LIST: {
-      auto b = std::make_unique<ListVectorBatch>(t.kind, cap);
+      auto b = std::make_unique<ListVectorBatch>(t.kind, cap, pool);
       b->elements = make_batch(r, r.getSubtypes(id)[0], cap, lazy, sel, tight);
       return b;
     }
     case ORCG_TYPE_MAP: {
-      auto b = std::make_unique<MapVectorBatch>(t.kind, cap);
+      auto b = std::make_unique<MapVectorBatch>(t.kind, cap, pool);
       const auto s = r.getSubtypes(id);
       b->keys = make_batch(r, s[0], cap, lazy, sel, tight);
       b->elements = make_batch(r, s[1], cap, lazy, sel, tight);
@@ -353,17 +599,17 @@ inline std::unique_ptr<ColumnVectorBatch> make_batch(const Reader& r, uint32_t i
     }
     case ORCG_TYPE_STRUCT: {
       // the selected fields only (Type::createRowBatch of the selected type)
-      auto b = std::make_unique<StructVectorBatch>(t.kind, cap);
+      auto b = std::make_unique<StructVectorBatch>(t.kind, cap, pool);
       for (uint32_t s : r.getSubtypes(id))
         if (sel(s)) b->fields.push_back(make_batch(r, s, cap, lazy, sel, tight));
       return b;
     }
     case ORCG_TYPE_UNION: {
-      auto b = std::make_unique<UnionVectorBatch>(t.kind, cap);
+      auto b = std::make_unique<UnionVectorBatch>(t.kind, cap, pool);
       for (uint32_t s : r.getSubtypes(id)) b->children.push_back(make_batch(r, s, cap, lazy, sel, tight));
       return b;
     }
-    default: return std::make_unique<LongVectorBatch>(t.kind, cap);
+    default: return std::make_unique<LongVectorBatch>(t.kind, cap, pool);
   }
 }
 
@@ -385,6 +631,16 @@ inline RowReader::RowReader(Reader& r, const RowReaderOptions& opts)
     o.include_len = nt;
   }
   r_.check(orcg_row_reader_create(r.get(), &o, &rr_));
+  // helper threads for the batch copies: ORCG_COPY_THREADS, else up to 3
+  // beside the caller's (a quarter of the host's threads)
+  unsigned helpers = 0;
+  if (const char* e = getenv("ORCG_COPY_THREADS")) {
+    helpers = (unsigned)std::max(0, atoi(e));
+  } else {
+    const unsigned hc = std::thread::hardware_concurrency();
+    helpers = std::min(3u, hc >= 8 ? hc / 4 : 0u);
+  }
+  pool_.reset(new CopyPool(helpers));
 }
 
 inline std::unique_ptr<ColumnVectorBatch> RowReader::createRowBatch(uint64_t capacity) const {
@@ -396,18 +652,21 @@ inline bool RowReader::next(ColumnVectorBatch& batch) {
   r_.check(orcg_row_reader_next(rr_, batch.capacity, &rows));
   batch.numElements = rows;
   if (rows == 0) return false;
+  copies_.clear();
   fill(0, batch);
+  pool_->run(copies_);
   return true;
 }
 
 inline void RowReader::seekToRow(uint64_t rowNumber) { r_.check(orcg_row_reader_seek_to_row(rr_, rowNumber)); }
 
 template <typename T, typename S>
-inline void narrow_copy(std::vector<T>& dst, const void* src, uint64_t n, uint64_t first) {
+inline void narrow_copy(DataBuffer<T>& dst, const void* src, uint64_t n, uint64_t first) {
   // static_cast<T> of the decoded values, as the reference's decoders narrow
   const S* p = (const S*)src + first;
   dst.resize(n);
-  for (uint64_t i = 0; i < n; ++i) dst[i] = static_cast<T>(p[i]);
+  T* d = dst.data();
+  for (uint64_t i = 0; i < n; ++i) d[i] = static_cast<T>(p[i]);
 }
 
 inline const std::vector<uint32_t>& RowReader::subs(uint32_t id, uint32_t kind) {
@@ -417,11 +676,13 @@ inline const std::vector<uint32_t>& RowReader::subs(uint32_t id, uint32_t kind) 
     const uint32_t nt = orcg_reader_num_types(r_.get());
     subs_.resize(nt);
     subs_known_.assign(nt, 0);
+    types_.resize(nt);
   }
   if (id >= subs_.size()) throw InvalidArgument("type id " + std::to_string(id) + " out of range");
   if (!subs_known_[id]) {
     for (uint32_t s : r_.getSubtypes(id))
       if (kind != ORCG_TYPE_STRUCT || isSelected(s)) subs_[id].push_back(s);
+    types_[id] = r_.getType(id);
     subs_known_[id] = 1;
   }
   return subs_[id];
@@ -436,115 +697,155 @@ inline void RowReader::new_stripe() {
   }
 }
 
+// One column of the batch (and its children): views point into the row
+// reader's host slab; bulk copies are queued (copies_, run by next()), the
+// per-row work (string pointers, offset rebasing, narrowing) done here.
 inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
   orcg_column_view v;
   uint64_t first = 0, n = 0;
   r_.check(orcg_row_reader_column(rr_, id, &v, &first, &n));
   if (!v.decoded)  // TIMESTAMP of a non-UTC writer zone (include/orcg_reader.h)
     throw InvalidArgument("column " + std::to_string(id) + " is not decoded by the GPU reader");
-  // the view points into the row reader's host slab: plain copies
   b.numElements = n;
   if (n > b.capacity) b.capacity = n;  // children grow like the reference's resize()
   b.hasNulls = v.has_nulls != 0;
-  if (b.hasNulls) Reader::hcopy(b.notNull, v.not_null, n, first);
-  else b.notNull.assign(n, 1);
+  // notNull is meaningful only when hasNulls (ColumnReader::next)
+  if (b.hasNulls) copy(b.notNull, v.not_null, n, first);
   const std::vector<uint32_t>& subs = this->subs(id, v.kind);
-  if (auto* l = dynamic_cast<LongVectorBatch*>(&b)) {
-    Reader::hcopy(l->data, v.data, n, first);
-  } else if (auto* i32 = dynamic_cast<IntVectorBatch*>(&b)) {
-    narrow_copy<int32_t, int64_t>(i32->data, v.data, n, first);
-  } else if (auto* i16 = dynamic_cast<ShortVectorBatch*>(&b)) {
-    narrow_copy<int16_t, int64_t>(i16->data, v.data, n, first);
-  } else if (auto* i8 = dynamic_cast<ByteVectorBatch*>(&b)) {
-    narrow_copy<int8_t, int64_t>(i8->data, v.data, n, first);
-  } else if (auto* d = dynamic_cast<DoubleVectorBatch*>(&b)) {
-    Reader::hcopy(d->data, v.data, n, first);
-  } else if (auto* f = dynamic_cast<FloatVectorBatch*>(&b)) {
-    narrow_copy<float, double>(f->data, v.data, n, first);
-  } else if (auto* e = dynamic_cast<EncodedStringVectorBatch*>(&b); e && v.index) {
-    // nextEncoded: index + the stripe's dictionary (ColumnReader.cc:596-607),
-    // one host dictionary per stripe shared by its batches
-    e->isEncoded = true;
-    Reader::hcopy(e->index, v.index, n, first);
-    new_stripe();
-    std::shared_ptr<StringDictionary>& dict = dicts_[id];
-    if (!dict) {
-      dict = std::make_shared<StringDictionary>();
-      Reader::hcopy(dict->dictionaryBlob, v.blob, v.blob_len);
-      Reader::hcopy(dict->dictionaryOffset, v.dict_offsets, v.dict_size + 1);
-    }
-    e->dictionary = dict;
-    e->data.assign(n, nullptr);
-    e->length.assign(n, 0);
-    for (uint64_t i = 0; i < n; ++i)
-      if (!b.hasNulls || b.notNull[i]) dict->getValueByIndex(e->index[i], e->data[i], e->length[i]);
-  } else if (auto* s = dynamic_cast<StringVectorBatch*>(&b)) {
-    const int64_t* start = (const int64_t*)v.data + first;  // the slab's (start, length) pairs
-    Reader::hcopy(s->length, v.length, n, first);
-    s->data.resize(n);
-    if (v.index) {
-      // dictionary: the stripe's blob, copied once and shared by its batches
-      new_stripe();
-      std::shared_ptr<std::vector<char>>& blob = blobs_[id];
-      if (!blob) {
-        blob = std::make_shared<std::vector<char>>();
-        Reader::hcopy(*blob, v.blob, v.blob_len);
-      }
-      s->blob.clear();
-      char* base = blob->data();
-      for (uint64_t i = 0; i < n; ++i) s->data[i] = base + (s->length[i] > 0 ? start[i] : 0);
-    } else {
-      // direct: the byte span the batch covers
-      uint64_t lo = ~0ull, hi = 0;
-      for (uint64_t i = 0; i < n; ++i)
-        if (s->length[i] > 0) {
-          lo = std::min<uint64_t>(lo, (uint64_t)start[i]);
-          hi = std::max<uint64_t>(hi, (uint64_t)(start[i] + s->length[i]));
+  const char* nn = b.hasNulls ? (const char*)v.not_null + first : nullptr;
+  switch (b.cls) {
+    case BatchClass::kLong: copy(static_cast<LongVectorBatch&>(b).data, v.data, n, first); break;
+    case BatchClass::kInt: narrow_copy<int32_t, int64_t>(static_cast<IntVectorBatch&>(b).data, v.data, n, first); break;
+    case BatchClass::kShort:
+      narrow_copy<int16_t, int64_t>(static_cast<ShortVectorBatch&>(b).data, v.data, n, first);
+      break;
+    case BatchClass::kByte: narrow_copy<int8_t, int64_t>(static_cast<ByteVectorBatch&>(b).data, v.data, n, first); break;
+    case BatchClass::kDouble: copy(static_cast<DoubleVectorBatch&>(b).data, v.data, n, first); break;
+    case BatchClass::kFloat: narrow_copy<float, double>(static_cast<FloatVectorBatch&>(b).data, v.data, n, first); break;
+    case BatchClass::kEncodedString:
+      if (v.index) {
+        // nextEncoded: index + the stripe's dictionary (ColumnReader.cc:596-607),
+        // one host dictionary per stripe shared by its batches
+        auto& e = static_cast<EncodedStringVectorBatch&>(b);
+        e.isEncoded = true;
+        copy(e.index, v.index, n, first);
+        new_stripe();
+        std::shared_ptr<StringDictionary>& dict = dicts_[id];
+        if (!dict) {
+          dict = std::make_shared<StringDictionary>(r_.getMemoryPool());
+          dict->dictionaryBlob.resize(v.blob_len);
+          if (v.blob_len) memcpy(dict->dictionaryBlob.data(), v.blob, v.blob_len);
+          dict->dictionaryOffset.resize(v.dict_size + 1);
+          memcpy(dict->dictionaryOffset.data(), v.dict_offsets, 8 * (v.dict_size + 1));
         }
-      if (lo == ~0ull) lo = hi = 0;
-      Reader::hcopy(s->blob, v.blob, hi - lo, lo);
-      for (uint64_t i = 0; i < n; ++i) s->data[i] = s->blob.data() + (s->length[i] > 0 ? start[i] - (int64_t)lo : 0);
+        e.dictionary = dict;
+        e.data.resize(n);
+        e.length.resize(n);
+        const int64_t* idx = (const int64_t*)v.index + first;
+        char** d = e.data.data();
+        int64_t* l = e.length.data();
+        for (uint64_t i = 0; i < n; ++i) {
+          if (nn && !nn[i]) {
+            d[i] = nullptr;
+            l[i] = 0;
+          } else {
+            dict->getValueByIndex(idx[i], d[i], l[i]);
+          }
+        }
+        break;
+      }
+      // an eager (non-dictionary) column in a lazy row reader
+      [[fallthrough]];
+    case BatchClass::kString: {
+      auto& s = static_cast<StringVectorBatch&>(b);
+      const int64_t* start = (const int64_t*)v.data + first;  // the slab's (start, length) pairs
+      const int64_t* len = (const int64_t*)v.length + first;
+      copy(s.length, v.length, n, first);
+      s.data.resize(n);
+      char** d = s.data.data();
+      if (v.index) {
+        // dictionary: the stripe's blob, copied once and shared by its batches
+        new_stripe();
+        std::shared_ptr<DataBuffer<char>>& blob = blobs_[id];
+        if (!blob) {
+          blob = std::make_shared<DataBuffer<char>>(r_.getMemoryPool(), v.blob_len);
+          if (v.blob_len) memcpy(blob->data(), v.blob, v.blob_len);
+        }
+        char* base = blob->data();
+        for (uint64_t i = 0; i < n; ++i) d[i] = base + (len[i] > 0 ? start[i] : 0);
+      } else {
+        // direct: the byte span the batch covers
+        uint64_t lo = ~0ull, hi = 0;
+        for (uint64_t i = 0; i < n; ++i)
+          if (len[i] > 0) {
+            lo = std::min<uint64_t>(lo, (uint64_t)start[i]);
+            hi = std::max<uint64_t>(hi, (uint64_t)(start[i] + len[i]));
+          }
+        if (lo == ~0ull) lo = hi = 0;
+        copy(s.blob, v.blob, hi - lo, lo);
+        char* base = s.blob.data();
+        for (uint64_t i = 0; i < n; ++i) d[i] = base + (len[i] > 0 ? start[i] - (int64_t)lo : 0);
+      }
+      break;
     }
-  } else if (auto* d64 = dynamic_cast<Decimal64VectorBatch*>(&b)) {
-    const orcg_type_info t = r_.getType(id);
-    d64->precision = (int32_t)t.precision;
-    d64->scale = (int32_t)t.scale;
-    Reader::hcopy(d64->values, v.data, n, first);
-  } else if (auto* d128 = dynamic_cast<Decimal128VectorBatch*>(&b)) {
-    const orcg_type_info t = r_.getType(id);
-    d128->precision = (int32_t)t.precision;
-    // Hive 0.11 decimals: the forced scale (DecimalHive11ColumnReader::next)
-    d128->scale = t.precision == 0 ? (int32_t)orcg_reader_hive11_scale(r_.get()) : (int32_t)t.scale;
-    Reader::hcopy(d128->values, v.data, n, first);  // [hi, lo] per value = Int128's layout
-  } else if (auto* ts = dynamic_cast<TimestampVectorBatch*>(&b)) {
-    Reader::hcopy(ts->data, v.data, n, first);
-    Reader::hcopy(ts->nanoseconds, v.secondary, n, first);
-  } else if (auto* lb = dynamic_cast<ListVectorBatch*>(&b)) {
-    Reader::hcopy(lb->offsets, v.offsets, n + 1, first);
-    const int64_t base = lb->offsets[0];
-    for (auto& o : lb->offsets) o -= base;
-    fill(subs[0], *lb->elements);
-  } else if (auto* mb = dynamic_cast<MapVectorBatch*>(&b)) {
-    Reader::hcopy(mb->offsets, v.offsets, n + 1, first);
-    const int64_t base = mb->offsets[0];
-    for (auto& o : mb->offsets) o -= base;
-    fill(subs[0], *mb->keys);
-    fill(subs[1], *mb->elements);
-  } else if (auto* sb = dynamic_cast<StructVectorBatch*>(&b)) {
-    for (size_t i = 0; i < subs.size(); ++i) fill(subs[i], *sb->fields[i]);
-  } else if (auto* ub = dynamic_cast<UnionVectorBatch*>(&b)) {
-    Reader::hcopy(ub->tags, v.tags, n, first);
-    std::vector<int64_t> offs;
-    Reader::hcopy(offs, v.offsets, n, first);
-    // offsets relative to each child's first row in this batch
-    std::vector<int64_t> base(subs.size(), -1);
-    for (uint64_t i = 0; i < n; ++i)
-      if ((!b.hasNulls || b.notNull[i]) && ub->tags[i] < subs.size() && base[ub->tags[i]] < 0)
-        base[ub->tags[i]] = offs[i];
-    ub->offsets.resize(n);
-    for (uint64_t i = 0; i < n; ++i)
-      ub->offsets[i] = (!b.hasNulls || b.notNull[i]) ? (uint64_t)(offs[i] - base[ub->tags[i]]) : 0;
-    for (size_t k = 0; k < subs.size(); ++k) fill(subs[k], *ub->children[k]);
+    case BatchClass::kDecimal64: {
+      auto& d64 = static_cast<Decimal64VectorBatch&>(b);
+      d64.precision = (int32_t)types_[id].precision;
+      d64.scale = (int32_t)types_[id].scale;
+      copy(d64.values, v.data, n, first);
+      break;
+    }
+    case BatchClass::kDecimal128: {
+      auto& d128 = static_cast<Decimal128VectorBatch&>(b);
+      d128.precision = (int32_t)types_[id].precision;
+      // Hive 0.11 decimals: the forced scale (DecimalHive11ColumnReader::next)
+      d128.scale = types_[id].precision == 0 ? (int32_t)orcg_reader_hive11_scale(r_.get()) : (int32_t)types_[id].scale;
+      copy(d128.values, v.data, n, first);  // [hi, lo] per value = Int128's layout
+      break;
+    }
+    case BatchClass::kTimestamp: {
+      auto& ts = static_cast<TimestampVectorBatch&>(b);
+      copy(ts.data, v.data, n, first);
+      copy(ts.nanoseconds, v.secondary, n, first);
+      break;
+    }
+    case BatchClass::kList:
+    case BatchClass::kMap: {
+      DataBuffer<int64_t>& offs =
+          b.cls == BatchClass::kList ? static_cast<ListVectorBatch&>(b).offsets : static_cast<MapVectorBatch&>(b).offsets;
+      const int64_t* src = (const int64_t*)v.offsets + first;
+      offs.resize(n + 1);
+      const int64_t base = src[0];
+      for (uint64_t i = 0; i <= n; ++i) offs[i] = src[i] - base;
+      if (b.cls == BatchClass::kList) {
+        fill(subs[0], *static_cast<ListVectorBatch&>(b).elements);
+      } else {
+        auto& mb = static_cast<MapVectorBatch&>(b);
+        fill(subs[0], *mb.keys);
+        fill(subs[1], *mb.elements);
+      }
+      break;
+    }
+    case BatchClass::kStruct: {
+      auto& sb = static_cast<StructVectorBatch&>(b);
+      for (size_t i = 0; i < subs.size(); ++i) fill(subs[i], *sb.fields[i]);
+      break;
+    }
+    case BatchClass::kUnion: {
+      auto& ub = static_cast<UnionVectorBatch&>(b);
+      const uint8_t* tags = (const uint8_t*)v.tags + first;
+      const int64_t* offs = (const int64_t*)v.offsets + first;
+      ub.tags.resize(n);
+      if (n) memcpy(ub.tags.data(), tags, n);
+      // offsets relative to each child's first row in this batch
+      std::vector<int64_t> base(subs.size(), -1);
+      for (uint64_t i = 0; i < n; ++i)
+        if ((!nn || nn[i]) && tags[i] < subs.size() && base[tags[i]] < 0) base[tags[i]] = offs[i];
+      ub.offsets.resize(n);
+      for (uint64_t i = 0; i < n; ++i) ub.offsets[i] = (!nn || nn[i]) ? (uint64_t)(offs[i] - base[tags[i]]) : 0;
+      for (size_t k = 0; k < subs.size(); ++k) fill(subs[k], *ub.children[k]);
+      break;
+    }
   }
 }
 

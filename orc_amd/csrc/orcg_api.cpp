@@ -209,6 +209,19 @@ int orcg_ctx_create(int device, orcg_ctx** out) {
   return ORCG_OK;
 }
 
+void* orcg_host_alloc(uint64_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void orcg_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
+}
+
 void orcg_ctx_destroy(orcg_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);

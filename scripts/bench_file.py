@@ -36,10 +36,12 @@ from workload_files import make_c3, make_c4, make_c5  # noqa: E402
 
 WORKLOADS = {
     "c3": (make_c3, 52 * 1920800, "configs[2]: demo-12-zlib schema at %d rows, zlib, %d MB stripes"),
-    "c4": (make_c4, 10_000_000, "configs[3] (one GPU's share): TPC-H lineitem-like 16 columns at %d rows, zstd, "
-                                "%d MB stripes"),
-    "c5": (make_c5, 10_000_000, "configs[4] (one GPU's share): struct<list<int>, map<string,int>> with 10%% nulls "
-                                "at %d rows, zstd, %d MB stripes"),
+    "c4": (make_c4, 10_000_000, "configs[3] schema (TPC-H lineitem-like 16 columns) at %d rows (one GPU's share of "
+                                "configs[3] is 1.25 * 10^8), zstd, %d MB stripes"),
+    "c5": (make_c5, 10_000_000, "configs[4] schema (struct<list<int>, map<string,int>>, 10%% nulls) at %d rows (one "
+                                "GPU's share of configs[4] is 1.25 * 10^7), zstd, %d MB stripes"),
+    "c1": (None, 0, "configs[0] substitute: examples/demo-11-zlib.orc (demo-11-none.orc is not in the reference), "
+                    "%d rows, full scan, %s"),
 }
 
 
@@ -140,7 +142,9 @@ def row_reader_leg(path, nrows, stripes_wall):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
+                    help="c1 = configs[0]'s scan of demo-11 (the zlib copy: demo-11-none.orc is not in the "
+                         "reference), RLEv1 streams; c3 / c4 / c5 = configs[2..4]")
     ap.add_argument("--rows", type=int, default=None)
     ap.add_argument("--stripe-mb", type=int, default=64)
     ap.add_argument("--path", default=None)
@@ -156,16 +160,21 @@ def main():
                          "host): device decode at steady clocks; 0 = skip")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; gloo lets "
                                                       "ranks share one GPU)")
+    ap.add_argument("--check", default="all", choices=["all", "first", "none"],
+                    help="stripes of this rank checked against pyarrow outside the timed region (numpy on the "
+                         "value buffers, tests/arrow_parity.py)")
     args = ap.parse_args()
     maker, default_rows, desc = WORKLOADS[args.workload]
     rows = args.rows or default_rows
     path = args.path or "/tmp/orcg_%s_%d.orc" % (args.workload, rows)
+    if args.workload == "c1":
+        path = args.path or os.path.join(ROOT, "tests", "golden", "files", "demo-11-zlib.orc")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     t0 = time.time()
-    if rank == 0 and not os.path.exists(path):
+    if rank == 0 and maker is not None and not os.path.exists(path):
         progress("writing %s (%d rows)" % (path, rows))
         maker(path + ".tmp", rows, args.stripe_mb)
         os.replace(path + ".tmp", path)
@@ -248,20 +257,26 @@ def main():
         concat = concat_leg(dist, r, path, first, last, rank)
 
     check = None
-    if last > first:
-        # correctness spot check on every rank: its first stripe against
-        # pyarrow (the reference C++ reader)
+    if last > first and args.check != "none":
+        # correctness check on every rank, outside the timed region: its
+        # stripes (all, or the first) against pyarrow (the reference's C++
+        # reader), compared buffer by buffer (tests/arrow_parity.py)
         import pyarrow.orc as po
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        from file_parity import first_difference
+        from arrow_parity import first_difference_arrow
 
-        progress("rank %d: checking stripe %d against pyarrow" % (rank, first))
-        got = r.read_stripe(first).to_pylist()
-        diff = first_difference(po.ORCFile(path).read_stripe(first).to_pylist(), got)
-        if diff:
-            raise SystemExit("%s stripe %d decode mismatch against pyarrow on rank %d: %s"
-                             % (args.workload, first, rank, diff))
-        check = "stripe %d (%d rows) equal to pyarrow" % (first, len(got))
+        pf = po.ORCFile(path)
+        todo = range(first, last) if args.check == "all" else range(first, first + 1)
+        checked = 0
+        for s in todo:
+            progress("rank %d: checking stripe %d against pyarrow" % (rank, s))
+            diff = first_difference_arrow(pf.read_stripe(s), r.read_stripe(s), r)
+            if diff:
+                raise SystemExit("%s stripe %d decode mismatch against pyarrow on rank %d: %s"
+                                 % (args.workload, s, rank, diff))
+            checked += int(stripe_rows[s])
+        check = "%s: stripes %d-%d (%d rows) equal to pyarrow (value buffers)" % (
+            "every stripe" if args.check == "all" else "first stripe", first, first + len(todo) - 1, checked)
 
     host = None
     if args.host_copy and rank == 0:
@@ -284,11 +299,13 @@ def main():
         import pyarrow.orc as po
         legs = []
         progress("pyarrow CPU legs")
+        reps = 5 if args.workload == "c1" else 1  # demo-11 reads in ~0.1 s: five reads per leg
         for th in [int(x) for x in args.cpu_threads.split(",") if x]:
             pa.set_cpu_count(th)
             t = time.perf_counter()
-            po.ORCFile(path).read()
-            tc = time.perf_counter() - t
+            for _ in range(reps):
+                po.ORCFile(path).read()
+            tc = (time.perf_counter() - t) / reps
             legs.append({"value": round(nrows / tc / 1e6, 2), "unit": "Mrows/s", "cores": th,
                          "kind": "pyarrow ORC C++ %s" % pa.__version__,
                          "sample": "full read of the same file to Arrow (pyarrow.orc.ORCFile.read), "
@@ -299,7 +316,8 @@ def main():
         line = {
             "metric": "file decode Mrows/s (host decompress -> H2D -> GPU decode into HBM)",
             "workload": args.workload,
-            "config": {"workload": desc % (nrows, args.stripe_mb), "stripes": r.num_stripes, "file_bytes": fsize,
+            "config": {"workload": desc % (nrows, "zlib, 385 stripes" if args.workload == "c1" else args.stripe_mb),
+                       "stripes": r.num_stripes, "file_bytes": fsize,
                        "n_gpus": world, "host_threads": int(os.environ.get("ORCG_HOST_THREADS", "0"))
                        or min(16, os.cpu_count() or 1)},
             "value": round(nrows / wall / 1e6, 2),

@@ -229,12 +229,13 @@ int main(int argc, char** argv) {
   uint64_t cap = 1024;
   std::vector<uint64_t> seeks;
   RowReaderOptions opts;
-  bool ranged = false, bench = false;
+  bool ranged = false, bench = false, pinned = false;
   for (int a = 2; a < argc; ++a) {
     if (!strcmp(argv[a], "--batch") && a + 1 < argc) cap = strtoull(argv[++a], nullptr, 10);
     else if (!strcmp(argv[a], "--lazy")) opts.setEnableLazyDecoding(true);
     else if (!strcmp(argv[a], "--tight")) opts.setUseTightNumericVector(true);
     else if (!strcmp(argv[a], "--bench")) bench = true;
+    else if (!strcmp(argv[a], "--pinned")) pinned = true;
     else if (!strcmp(argv[a], "--include") && a + 1 < argc) {
       std::list<uint64_t> ids;
       char* p = argv[++a];
@@ -258,7 +259,12 @@ int main(int argc, char** argv) {
   }
   try {
     Context ctx(0);
-    Reader reader(ctx, argv[1]);
+    // --pinned: batches in page-locked memory from the caller's pool
+    // (ReaderOptions::setMemoryPool, the orc::MemoryPool seam)
+    PinnedMemoryPool pinned_pool;
+    ReaderOptions ropts;
+    if (pinned) ropts.setMemoryPool(pinned_pool);
+    Reader reader(ctx, argv[1], ropts);
     auto rows = reader.createRowReader(opts);
     g_rows = rows.get();
     g_names.assign(orcg_reader_num_types(reader.get()), {});

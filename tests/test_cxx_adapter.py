@@ -243,3 +243,22 @@ def test_two_row_readers_keep_their_own_options():
     assert rows_b == [{"long1": x["long1"]} for x in full]
     assert a.is_selected(ids["int1"]) and not a.is_selected(ids["long1"])
     assert np.all([b.is_selected(ids["long1"]), not b.is_selected(ids["int1"])])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["TestOrcFile.testSeek.orc", "TestOrcFile.testUnionAndTimestamp.orc",
+                                  "TestStringDictionary.testRowIndex.orc"])
+def test_row_reader_adapter_pinned_memory_pool(name):
+    """ReaderOptions::setMemoryPool (Reader.hh:123, MemoryPool.hh:27-33): the
+    batches and dictionaries allocated from the caller's pool, here
+    PinnedMemoryPool (page-locked memory from orcg_host_alloc); every row
+    against the reference's expected output, capacities 1000 and 1024, with
+    the batch copies spread over the copy pool's helper threads."""
+    from file_parity import printer_equal
+
+    inc, want = _include(name)
+    for batch in (1000, 1024):
+        got = _run_reader(name, "--batch", batch, "--include", inc, "--pinned")
+        assert len(got) == len(want)
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert printer_equal(w, g), (name, batch, i, w, g)
