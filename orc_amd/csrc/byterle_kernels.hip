@@ -120,7 +120,8 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
                                                             const uint64_t* __restrict__ segtab, uint64_t nsegs,
                                                             uint64_t begin, uint64_t nout, uint8_t* __restrict__ dst,
                                                             unsigned long long* err,
-                                                            unsigned long long* __restrict__ ones_total) {
+                                                            unsigned long long* __restrict__ ones_total,
+                                                            const uint64_t* __restrict__ d_nout) {
 #ifdef ORCG_PHASE_PROF
   uint64_t prof_last_ = wall_clock64();
 #endif
@@ -135,7 +136,7 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
   const uint64_t g = blockIdx.x;
   const int tid = (int)threadIdx.x;
   const int lane = tid % kWave, wave = tid / kWave;
-  const uint64_t end = begin + nout;
+  const uint64_t end = begin + (d_nout ? *d_nout : nout);
   const uint64_t scale = kBool ? 8 : 1;  // output units per decoded byte
   const uint64_t vend = (end + scale - 1) / scale;  // decoded bytes needed: index < vend
   const uint64_t seg_start = segtab[2 * g];
@@ -345,16 +346,17 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
 }  // namespace
 
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
-                   bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst, uint64_t* d_ones) {
+                   bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst, uint64_t* d_ones,
+                   const uint64_t* d_nout) {
   if (nsegs == 0 || nout == 0) return ORCG_OK;
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   const dim3 grid((unsigned)nsegs), block(kBThreads);
   if (boolean)
     hipLaunchKernelGGL(byterle_kernel<true>, grid, block, 0, ctx->stream, d_src, src_len, d_segtab, nsegs, begin,
-                       nout, d_dst, ctx->d_err, (unsigned long long*)d_ones);
+                       nout, d_dst, ctx->d_err, (unsigned long long*)d_ones, d_nout);
   else
     hipLaunchKernelGGL(byterle_kernel<false>, grid, block, 0, ctx->stream, d_src, src_len, d_segtab, nsegs, begin,
-                       nout, d_dst, ctx->d_err, (unsigned long long*)nullptr);
+                       nout, d_dst, ctx->d_err, (unsigned long long*)nullptr, d_nout);
   return hip_check(ctx, hipGetLastError(), "byterle_kernel launch");
 }
 

@@ -80,6 +80,7 @@ struct RleJob {
   uint32_t is_signed;
   uint32_t pad;
   unsigned long long* err;  // the job's device error record (the reader's per-column word), or null = the launch's
+  const uint64_t* dcount;   // non-null: the value count on the device (nvalues is then the output's capacity)
 };
 
 int set_error(Ctx* ctx, int status, const std::string& msg);
@@ -102,11 +103,12 @@ bool rlev2_variant_valid(int v);
 // split > 1: nsegs x split workgroups, each decoding 1/split of its
 // segment's values (segments too few to fill the GPU: a file's child-column
 // row groups); 0 = by the segments' count and size (auto_split); the
-// queueing instances (variants 3, 7) ignore it
+// queueing instances (variants 3, 7) ignore it. d_count (may be null): the
+// value count on the device, nvalues then bounds the output only.
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
-                       void* d_dst, int dst_bytes, uint32_t split = 0);
+                       void* d_dst, int dst_bytes, uint32_t split = 0, const uint64_t* d_count = nullptr);
 
 // Every stream of `jobs` (segment-table mode, int64 output) in one launch per
 // instance the default's density rule picks (or the pinned variant);
@@ -116,9 +118,11 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs);
 bool rlev2_multi_capable(int variant);
 
 // d_ones (boolean mode, may be null): += the set rows written (a PRESENT
-// stream's non-null rows), one atomic per wave
+// stream's non-null rows), one atomic per wave. d_nout (may be null): the
+// output count on the device (nout then bounds the output only).
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
-                   bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst, uint64_t* d_ones = nullptr);
+                   bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst, uint64_t* d_ones = nullptr,
+                   const uint64_t* d_nout = nullptr);
 int launch_rlev1(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed, const uint64_t* d_segtab,
                  uint64_t nsegs, uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes);
 int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,

@@ -174,6 +174,9 @@ struct Col {
   int64_t* index = nullptr;      // dictionary strings: entry of each row (EncodedStringVectorBatch::index)
   int64_t* dict_offsets = nullptr;  // dictionary strings: dict_size + 1 entry offsets (StringDictionary)
   StreamBuf s[5];  // PRESENT, DATA, LENGTH, DICTIONARY_DATA, SECONDARY
+  // has_nulls is provisional until the stripe's checks run: the non-null
+  // count stayed on the device (orcg_reader::device_counts)
+  bool nulls_deferred = false;
 };
 
 enum { kSlotPresent = 0, kSlotData = 1, kSlotLength = 2, kSlotDict = 3, kSlotSecondary = 4 };
@@ -381,7 +384,16 @@ struct orcg_reader {
   int prepare(uint64_t s, HostStage& hs) const;
   int read_stripes(uint64_t first, uint64_t count);
   int upload_and_decode(HostStage& hs, DevSlot& ds);
-  int decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count, const int64_t* rg_rows);
+  // d_in_count (may be null): in_count is on the device (the parent's
+  // non-null rows), in_count is then an upper bound; in_col: the column whose
+  // mask in_nn is
+  int decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count, const int64_t* rg_rows,
+             const uint64_t* d_in_count = nullptr, Col* in_col = nullptr);
+  // Columns whose value streams take a device-resident value count (RLEv2
+  // through the tiled instances): their PRESENT decode's non-null count is
+  // not read back mid-stripe (one stream synchronisation per nullable column
+  // saved); has_nulls is settled with the stripe's checks.
+  bool device_counts(const Col& c) const;
   // row-group context of the column being decoded (segments())
   const int64_t* cur_rows = nullptr;  // device: first row of each row group, in the column's rows
   uint64_t cur_n = 0;
@@ -392,7 +404,9 @@ struct orcg_reader {
   // DictionaryLoader.hh:42) unless force_v2 (Decimal64ColumnReaderV2 is always RLEv2)
   // (*out: the stream's values, decoded by this stripe's multi-stream batch
   // when collect() queued it, else allocated and decoded now)
-  int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** out, bool force_v2 = false);
+  // (dcount: the value count on the device, `count` then only sizes the output)
+  int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** out, bool force_v2 = false,
+                 const uint64_t* dcount = nullptr);
   // Multi-stream batch: before decode(), the RLEv2 streams whose value
   // counts and segments are known without device results (columns with no
   // PRESENT stream, under parents with none) are queued and decoded by one
@@ -403,7 +417,8 @@ struct orcg_reader {
   std::unordered_map<uint64_t, std::pair<int64_t*, uint64_t>> batched;  // (column, slot) -> (values, count)
   int queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2);
   int collect(uint32_t id, uint64_t n, const int64_t* rg_rows);
-  int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones = nullptr);
+  int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones = nullptr,
+                  const uint64_t* d_count = nullptr);
   int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
   template <typename T>
   T* alloc(uint64_t count) {
@@ -503,7 +518,20 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
   return ORCG_OK;
 }
 
-int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** pout, bool force_v2) {
+bool orcg_reader::device_counts(const Col& c) const {
+  static const bool off = getenv("ORCG_SYNC_COUNTS") != nullptr;  // A/B: the synchronous counts
+  if (off || !rlev2_multi_capable(ctx->rlev2_variant)) return false;
+  const uint32_t k = c.kind;
+  if (k == ORCG_TYPE_STRUCT) return true;
+  if (c.encoding == kDirect || c.encoding == kDictionary) return false;  // RLEv1
+  if (is_int_kind(k) || k == ORCG_TYPE_LIST || k == ORCG_TYPE_MAP || k == ORCG_TYPE_TIMESTAMP ||
+      k == ORCG_TYPE_TIMESTAMP_INSTANT)
+    return true;
+  return is_string_kind(k) && c.encoding == kDictionaryV2;
+}
+
+int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** pout, bool force_v2,
+                            const uint64_t* dcount) {
   const uint64_t key = (uint64_t)(&c - H->cols.data()) * 8 + (uint64_t)slot;
   const auto it = batched.find(key);
   if (it != batched.end() && it->second.second == count) {
@@ -517,7 +545,8 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   if (count == 0) return ORCG_OK;
   if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
   const bool v1 = !force_v2 && (c.encoding == kDirect || c.encoding == kDictionary);
-  if (!sb.pos && count > sb.plan->values) {
+  // (with a device count the kernel reports a stream short of values)
+  if (!dcount && !sb.pos && count > sb.plan->values) {
     const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)(v1 ? kErrV1BadRead : kErrBadRead);
     return fail(dev_error_status(e), dev_error_message(e));
   }
@@ -530,7 +559,8 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   if (v1)
     rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
   else
-    rc = launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
+    rc = dcount ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, 0, dcount)
+                : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
 
@@ -606,11 +636,12 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
   return rc;
 }
 
-int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones) {
+int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones,
+                             const uint64_t* d_count) {
   StreamBuf& sb = c.s[slot];
   if (count == 0) return ORCG_OK;
   if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
-  if (!sb.pos) {
+  if (!sb.pos && !d_count) {  // (with a device count the kernel reports a short stream)
     const uint64_t avail = boolean ? sb.plan->values * 8 : sb.plan->values;
     if (count > avail) {
       const uint32_t e = sb.plan->err != kErrNone ? sb.plan->err : (uint32_t)kErrByteBadRead;
@@ -621,12 +652,13 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   uint64_t nseg;
   int rc = segments(c, slot, boolean, &d_seg, &nseg);
   if (rc) return rc;
-  rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones);
+  rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count);
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
 
 
-int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count, const int64_t* rg_rows) {
+int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t in_count, const int64_t* rg_rows,
+                        const uint64_t* d_in_count, Col* in_col) {
   Col& c = H->cols[id];
   if (!selected[id] || !c.supported) return ORCG_OK;
   // this column's kernels report into its own device error record
@@ -649,27 +681,66 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   cur_in_nn = in_nn;
   cur_row_nn = nullptr;
   // ColumnReader::next: PRESENT bits for the incoming non-null rows
-  uint64_t nonnull = in_nn ? in_count : n;
+  // (d_in: their count is on the device, in_count an upper bound)
+  const bool dev = device_counts(c);
+  const uint64_t* d_in = in_nn ? d_in_count : nullptr;
+  if (d_in && !dev) {  // this column needs the incoming count on the host
+    if ((rc = read_back({d_in}, &in_count))) return rc;
+    d_in = nullptr;
+  }
+  uint64_t nonnull = in_nn ? in_count : n;  // exact, or (d_nonnull) an upper bound
+  const uint64_t* d_nonnull = d_in;
   uint8_t* nn = nullptr;
   if (c.s[kSlotPresent].present) {
     ORCG_ALLOC(uint8_t, bits, in_count + 8);
     // the decode counts the set rows it writes: the non-null rows, with or
     // without the parent's mask scattered in
     uint64_t* ones = D->d_ones + id;
-    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits, ones))) return rc;
+    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits, ones, d_in))) return rc;
     if (in_nn) {
       ORCG_ALLOC_TO(uint8_t, nn, n);
       if ((rc = scatter(bits, in_nn, n, nn, 1))) return fail_ctx(rc);
     } else {
       nn = bits;
     }
-    if ((rc = read_back({ones}, &nonnull))) return rc;
+    if (dev) {
+      nonnull = n;
+      d_nonnull = ones;
+    } else {
+      if ((rc = read_back({ones}, &nonnull))) return rc;
+      d_nonnull = nullptr;
+    }
   } else if (in_nn) {
     nn = const_cast<uint8_t*>(in_nn);
   }
-  c.has_nulls = nn != nullptr && nonnull < n;
+  c.has_nulls = nn != nullptr && (d_nonnull != nullptr || nonnull < n);
   if (in_nn && !c.s[kSlotPresent].present) c.has_nulls = true;  // incoming mask copied (:97-101)
   c.nn = c.has_nulls ? nn : nullptr;
+  // provisional has_nulls: settled by the stripe's checks (column order:
+  // a parent's before its children's)
+  if (c.s[kSlotPresent].present && d_nonnull) {
+    const uint64_t* h = defer(d_nonnull, 1);
+    if (!h) return fail(ORCG_DEVICE_ERROR, "D2H of the non-null count failed");
+    c.nulls_deferred = true;
+    Col* cp = &c;
+    checks.emplace_back(cur_col, [cp, h, n]() -> int {
+      if (*h >= n) {
+        cp->has_nulls = false;
+        cp->nn = nullptr;
+      }
+      return ORCG_OK;
+    });
+  } else if (in_nn && !c.s[kSlotPresent].present && in_col && in_col->nulls_deferred) {
+    c.nulls_deferred = true;
+    Col* cp = &c;
+    checks.emplace_back(cur_col, [cp, in_col]() -> int {
+      if (!in_col->has_nulls) {  // the parent had no nulls after all: no mask was passed down
+        cp->has_nulls = false;
+        cp->nn = nullptr;
+      }
+      return ORCG_OK;
+    });
+  }
   const uint8_t* row_nn = c.nn;
   cur_row_nn = row_nn;
 
@@ -760,14 +831,14 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Timestamp column");
     if (!has_sec) return fail(ORCG_PARSE_ERROR, "SECONDARY stream not found in Timestamp column");
     int64_t *secs, *nanos;
-    if ((rc = int_stream(c, kSlotData, true, nonnull, &secs))) return rc;
-    if ((rc = int_stream(c, kSlotSecondary, false, nonnull, &nanos))) return rc;
+    if ((rc = int_stream(c, kSlotData, true, nonnull, &secs, false, d_nonnull))) return rc;
+    if ((rc = int_stream(c, kSlotSecondary, false, nonnull, &nanos, false, d_nonnull))) return rc;
     if ((rc = launch_timestamp(ctx, secs, nanos, nonnull, kOrcEpochUtc))) return fail_ctx(rc);
     if (!(c.data = place_i64(secs)) || !(c.secondary = place_i64(nanos))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (is_int_kind(k)) {
     if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Integer column");
     int64_t* dense;
-    if ((rc = int_stream(c, kSlotData, true, nonnull, &dense))) return rc;
+    if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, false, d_nonnull))) return rc;
     if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (k == ORCG_TYPE_BOOLEAN || k == ORCG_TYPE_BYTE) {
     if (!has_data)
@@ -837,7 +908,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDictionaryColumn");
       c.blob = db.present ? D->d_stage + db.host_off : nullptr;
       int64_t* idx;
-      if ((rc = int_stream(c, kSlotData, false, nonnull, &idx))) return rc;
+      if ((rc = int_stream(c, kSlotData, false, nonnull, &idx, false, d_nonnull))) return rc;
       int64_t* ridx = idx;
       if (row_nn) {
         ORCG_ALLOC_TO(int64_t, ridx, n);
@@ -885,7 +956,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_LIST ? "LENGTH stream not found in List column"
                                                         : "LENGTH stream not found in Map column");
     int64_t* dlen;
-    if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen))) return rc;
+    if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false, d_nonnull))) return rc;
     int64_t* rlen = dlen;
     if (row_nn) {
       ORCG_ALLOC_TO(int64_t, rlen, n);
@@ -906,7 +977,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if ((rc = decode(st, total, nullptr, total, child_rows))) return rc;
   } else if (k == ORCG_TYPE_STRUCT) {
     for (uint32_t st : footer.types[id].subtypes)
-      if ((rc = decode(st, n, c.nn, nonnull, rg_rows))) return rc;
+      if ((rc = decode(st, n, c.nn, nonnull, rg_rows, c.nn ? d_nonnull : nullptr, &c))) return rc;
   } else if (k == ORCG_TYPE_UNION) {
     // UnionColumnReader (ColumnReader.cc:1158-1274): byte-RLE tags for the
     // non-null rows; each row's offset is its rank among the rows of its

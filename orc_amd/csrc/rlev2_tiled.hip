@@ -1530,7 +1530,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint64_t* __restrict__ p_segtab, uint64_t p_nsegs, uint64_t rows_per_group,
     uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* p_err,
     unsigned long long* __restrict__ defer_q, uint32_t defer_par, const RleJob* __restrict__ jobs,
-    uint32_t njobs, uint32_t p_split) {
+    uint32_t njobs, uint32_t p_split, const uint64_t* __restrict__ p_dcount) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
@@ -1603,7 +1603,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   const int64_t* rows = nullptr;
   uint64_t nsegs = p_nsegs;
   uint64_t value_begin = p_value_begin;
-  uint64_t value_end = p_value_begin + p_nvalues;
+  // (p_dcount: the value count lives on the device, e.g. a nullable
+  // column's non-null rows counted by its PRESENT decode; p_nvalues is then
+  // only the output's capacity)
+  uint64_t value_end = p_value_begin + (p_dcount ? uni64(*p_dcount) : p_nvalues);
   T* dst = p_dst;
   unsigned long long* err = p_err;
   auto bind = [&](const uint64_t gg) -> uint64_t {
@@ -1623,7 +1626,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     rows = (const int64_t*)uni64((uint64_t)(uintptr_t)J->rows);
     nsegs = uni64(J->nsegs);
     value_begin = 0;
-    value_end = uni64(J->nvalues);
+    const uint64_t jdc = uni64((uint64_t)(uintptr_t)J->dcount);
+    value_end = jdc ? uni64(*(const uint64_t*)(uintptr_t)jdc) : uni64(J->nvalues);
     dst = (T*)uni64((uint64_t)(uintptr_t)J->dst);
     const uint64_t je = uni64((uint64_t)(uintptr_t)J->err);
     err = je ? (unsigned long long*)(uintptr_t)je : p_err;
@@ -2161,7 +2165,7 @@ static int default_variant(uint64_t src_len, uint64_t est_values) {
 static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode, uint64_t rows_per_group,
                         uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes, const RleJob* jobs_d,
-                        uint32_t njobs_d, uint32_t split = 1) {
+                        uint32_t njobs_d, uint32_t split = 1, const uint64_t* dcount = nullptr) {
   if (nsegs == 0 || nvalues == 0) return ORCG_OK;
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   if (dst_bytes != 8 && dst_bytes != 4 && dst_bytes != 2)
@@ -2188,7 +2192,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
   hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
                      d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
-                     ctx->d_err, dq, dpar, jobs_d, njobs_d, sp)
+                     ctx->d_err, dq, dpar, jobs_d, njobs_d, sp, dcount)
 // single-stream instances (+ the multi-stream one for the default's
 // instances, ORCG_KX; the tuning variants have none, ORCG_KX1)
 #define ORCG_KX1(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                 \
@@ -2317,7 +2321,7 @@ static uint32_t auto_split(uint64_t nsegs, uint64_t values) {
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
-                       int dst_bytes, uint32_t split) {
+                       int dst_bytes, uint32_t split, const uint64_t* d_count) {
   int variant = ctx->rlev2_variant;
   const uint64_t est = positions_mode ? nsegs * rows_per_group : nvalues;
   if (split == 0) split = auto_split(nsegs, est);
@@ -2328,7 +2332,7 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
     if (split > 1 && variant == 3) variant = 6;
   }
   return launch_tiled(ctx, variant, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode, rows_per_group,
-                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, split);
+                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, split, d_count);
 }
 
 // Job tables go through a pinned ring mirrored on the device: entries are
