@@ -144,16 +144,27 @@ __global__ void dict_gather_kernel(const T* __restrict__ idx, const uint8_t* __r
   }
 }
 
+// Dictionary offsets: exclusive scan of the entry lengths (one workgroup).
+// With `summary`: [0] = the blob bytes (offsets[n]), [1] = 1 if an entry
+// length is negative (loadStringDictionary's check, DictionaryLoader.cc:71-77)
+// -- the file reader's whole dictionary preparation in one launch.
 __global__ __launch_bounds__(1024) void lengths_scan_kernel(const int64_t* __restrict__ lengths, uint64_t n,
-                                                             int64_t* __restrict__ offsets) {
+                                                             int64_t* __restrict__ offsets,
+                                                             uint64_t* __restrict__ summary) {
   __shared__ uint64_t wsum[1024 / kWave];
   __shared__ uint64_t carry_s;
+  __shared__ uint32_t neg_s;
   const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
-  if (threadIdx.x == 0) carry_s = 0;
+  if (threadIdx.x == 0) {
+    carry_s = 0;
+    neg_s = 0;
+  }
   __syncthreads();
+  bool neg = false;
   for (uint64_t b = 0; b < n; b += 1024) {
     const uint64_t i = b + threadIdx.x;
     const uint64_t x = i < n ? (uint64_t)lengths[i] : 0;
+    neg |= (int64_t)x < 0;
     const uint64_t inc = wave_inclusive_scan(x, lane);
     if (lane == kWave - 1) wsum[wv] = inc;
     __syncthreads();
@@ -164,7 +175,15 @@ __global__ __launch_bounds__(1024) void lengths_scan_kernel(const int64_t* __res
     if (threadIdx.x == 1023) carry_s = before + inc;
     __syncthreads();
   }
-  if (threadIdx.x == 0) offsets[n] = (int64_t)carry_s;
+  if (summary && __any(neg) && lane == 0) atomicOr(&neg_s, 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    offsets[n] = (int64_t)carry_s;
+    if (summary) {
+      summary[0] = carry_s;
+      summary[1] = neg_s;
+    }
+  }
 }
 
 // Multi-workgroup exclusive scan of int64 values (lengths -> offsets):
@@ -405,8 +424,10 @@ int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t 
   return hip_check(ctx, hipGetLastError(), "scatter launch");
 }
 
-int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets) {
-  hipLaunchKernelGGL(lengths_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, d_lengths, dict_size, d_offsets);
+int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets,
+                        uint64_t* d_summary) {
+  hipLaunchKernelGGL(lengths_scan_kernel, dim3(1), dim3(1024), 0, ctx->stream, d_lengths, dict_size, d_offsets,
+                     d_summary);
   return hip_check(ctx, hipGetLastError(), "dictionary offsets launch");
 }
 

@@ -127,7 +127,9 @@ int launch_rlev1(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed
                  uint64_t nsegs, uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes);
 int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,
                    int fill_mode, int64_t fill);
-int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets);
+// (d_summary, may be null: [0] blob bytes, [1] any negative length)
+int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, int64_t* d_offsets,
+                        uint64_t* d_summary = nullptr);
 int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t* d_nn, uint64_t n,
                        const int64_t* d_offsets, uint64_t dict_size, int64_t* d_start, int64_t* d_len);
 

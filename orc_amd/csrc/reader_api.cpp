@@ -887,11 +887,18 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       int64_t* dlen;
       ORCG_ALLOC(int64_t, doff, dict_size + 1);
       if ((rc = int_stream(c, kSlotLength, false, dict_size, &dlen))) return rc;
-      if ((rc = launch_flag_negative(ctx, dlen, dict_size, D->d_scalars + 1))) return fail_ctx(rc);
-      if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
-      if ((rc = hip_check(ctx, hipMemcpyAsync(D->d_scalars, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream), "copy")))
-        return fail_ctx(rc);
-      const uint64_t* h = defer(D->d_scalars, 2);  // blob bytes, negative-length flag
+      ORCG_ALLOC(uint64_t, summary, 2);  // blob bytes, negative-length flag
+      if (dict_size <= 65536) {
+        // offsets, blob size and the negative-length check in one launch
+        if ((rc = launch_dict_offsets(ctx, dlen, dict_size, doff, summary))) return fail_ctx(rc);
+      } else {
+        if ((rc = launch_flag_negative(ctx, dlen, dict_size, summary + 1))) return fail_ctx(rc);
+        if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
+        if ((rc = hip_check(ctx, hipMemcpyAsync(summary, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream),
+                            "copy")))
+          return fail_ctx(rc);
+      }
+      const uint64_t* h = defer(summary, 2);
       if (!h) return fail(ORCG_DEVICE_ERROR, "D2H of the dictionary size failed");
       StreamBuf& db = c.s[kSlotDict];
       Col* cp = &c;
