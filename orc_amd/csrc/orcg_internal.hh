@@ -100,15 +100,12 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
 // 1 wave-walk, and pins of single tiled instances (launch_rlev2_tiled).
 constexpr int kMaxRlev2Variant = 39;
 bool rlev2_variant_valid(int v);
-// split > 1: nsegs x split workgroups, each decoding 1/split of its
-// segment's values (segments too few to fill the GPU: a file's child-column
-// row groups); 0 = by the segments' count and size (auto_split); the
-// queueing instances (variants 3, 7) ignore it. d_count (may be null): the
-// value count on the device, nvalues then bounds the output only.
+// d_count (may be null): the value count on the device, nvalues then
+// bounds the output only.
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
-                       void* d_dst, int dst_bytes, uint32_t split = 0, const uint64_t* d_count = nullptr);
+                       void* d_dst, int dst_bytes, const uint64_t* d_count = nullptr);
 
 // Every stream of `jobs` (segment-table mode, int64 output) in one launch per
 // instance the default's density rule picks (or the pinned variant);
@@ -177,12 +174,12 @@ int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out);
 inline int launch_rlev2(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                         uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
-                        void* d_dst, int dst_bytes, uint32_t split = 0) {
+                        void* d_dst, int dst_bytes) {
   if (ctx->rlev2_variant == ORCG_RLEV2_WAVE_WALK)
     return launch_rlev2_decode(ctx, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode,
                                rows_per_group, value_begin, nvalues, d_dst, dst_bytes);
   return launch_rlev2_tiled(ctx, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode,
-                            rows_per_group, value_begin, nvalues, d_dst, dst_bytes, split);
+                            rows_per_group, value_begin, nvalues, d_dst, dst_bytes);
 }
 
 }  // namespace orcg

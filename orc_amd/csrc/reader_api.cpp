@@ -559,7 +559,7 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   if (v1)
     rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
   else
-    rc = dcount ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, 0, dcount)
+    rc = dcount ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, dcount)
                 : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
   return rc ? fail_ctx(rc) : ORCG_OK;
 }

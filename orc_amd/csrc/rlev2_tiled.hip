@@ -1384,30 +1384,22 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     const uint32_t Ls = shortr ? run.L : 0u;
     const uint32_t incl = wave_scan_u32(Ls);
     constexpr bool kStraight = (kOpt & kOptDirect) != 0;
-    // every run parsed here is expanded before the next 64 are parsed: runs
-    // of consecutive short runs through the stage (or straight), each long
-    // / PATCHED_BASE run by the whole wave (a mix of short and long runs,
-    // e.g. low-cardinality dictionary indices, parsed its 64 headers again
-    // after every long run)
+    // every run parsed here is expanded before the next 64 are parsed
+    // (a mix of short and long runs, e.g. low-cardinality dictionary
+    // indices, used to parse its 64 headers again after every long run):
+    // first the runs of consecutive short runs, through the stage (or
+    // straight), then each long / PATCHED_BASE run by the whole wave, once
+    // the parsed runs are dead (fewer live registers around expand_run)
     const uint32_t nact = r1 - c < (uint32_t)kWave ? r1 - c : (uint32_t)kWave;
-    const uint64_t shortm = __ballot(shortr);
-    uint32_t a = 0;
-    while (a < nact) {
-      if (!((shortm >> a) & 1ull)) {
-#ifdef ORCG_DEBUG_COVER
-        if (lane == 0) ORCG_COVER_ADD(parse_run([&](uint32_t i) { return lds_byte(win, uni(s_off[c + a]) + i); }, ~0ull,
-                                                kHdrLim, is_signed).L);
-#endif
-        expand_run<kOpt>(win, nwords, uni(s_off[c + a]), vi + uni(s_val[c + a]), is_signed, value_begin, value_end,
-                         dst, lane);
-        ++a;
-        continue;
-      }
+    const uint64_t longm = __ballot(act && !shortr);
+    for (uint64_t rem = __ballot(shortr); rem;) {
+      const uint32_t a = (uint32_t)__builtin_ctzll(rem);
       // short runs [a, b): consecutive in the output; a stage-full at most
       const uint32_t base = a ? rdlane(incl, a - 1) : 0u;
       const uint64_t stop_m = __ballot((uint32_t)lane >= a && (!shortr || (!kStraight && incl - base > kStage)));
       uint32_t b = stop_m ? (uint32_t)__builtin_ctzll(stop_m) : (uint32_t)kWave;
       if (b > nact) b = nact;
+      rem &= b >= (uint32_t)kWave ? 0ull : ~((1ull << b) - 1ull);
       const bool mine = (uint32_t)lane >= a && (uint32_t)lane < b;
       const uint32_t myl = mine ? Ls : 0u;
       ORCG_COVER_ADD(myl);
@@ -1427,7 +1419,6 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
             if (j < myl && g >= value_begin && g < value_end) store1<kOpt>(dst + (g - value_begin), x);
           }
         }
-        a = b;
         continue;
       }
       const uint32_t st0 = incl - Ls - base;
@@ -1449,7 +1440,15 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      a = b;
+    }
+    for (uint64_t m = longm; m; m &= m - 1) {
+      const uint32_t a = (uint32_t)__builtin_ctzll(m);
+#ifdef ORCG_DEBUG_COVER
+      if (lane == 0) ORCG_COVER_ADD(parse_run([&](uint32_t i) { return lds_byte(win, uni(s_off[c + a]) + i); }, ~0ull,
+                                              kHdrLim, is_signed).L);
+#endif
+      expand_run<kOpt>(win, nwords, uni(s_off[c + a]), vi + uni(s_val[c + a]), is_signed, value_begin, value_end, dst,
+                       lane);
     }
     c += nact;
   }
@@ -1530,7 +1529,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint64_t* __restrict__ p_segtab, uint64_t p_nsegs, uint64_t rows_per_group,
     uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* p_err,
     unsigned long long* __restrict__ defer_q, uint32_t defer_par, const RleJob* __restrict__ jobs,
-    uint32_t njobs, uint32_t p_split, const uint64_t* __restrict__ p_dcount) {
+    uint32_t njobs, const uint64_t* __restrict__ p_dcount) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
@@ -1634,10 +1633,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     return gg - uni64(J->seg_base);
   };
 
-  // split launches (p_split > 1): workgroup split_k of split_n decodes only
-  // its share of the segment's values (whole 512-value blocks); it walks the
-  // runs before its share, but expands only its own
-  uint32_t split_k = 0, split_n = 1;
   // one segment, from its start or (queued) from a byte offset / value index
   auto run_segment = [&](const uint64_t gg, const bool queued, const uint64_t q_pos, const uint64_t q_vi) {
   const uint64_t g = bind(gg);
@@ -1660,22 +1655,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   if (g + 1 < nsegs) v_next = seg_at(g + 1, &seg_end);
   if (seg_end > src_len) seg_end = src_len;
   if (vi >= value_end || v_next <= value_begin) return;
-  if (split_n > 1) {
-    const uint64_t lo = vi > value_begin ? vi : value_begin;
-    const uint64_t hi = v_next < value_end ? v_next : value_end;
-    uint64_t q = (hi - lo + split_n - 1) / split_n;
-    q = (q + 511) & ~511ull;
-    const uint64_t a = lo + (uint64_t)split_k * q;
-    const uint64_t b = a + q < hi ? a + q : hi;
-    if (a < b) {
-      dst += (a - value_begin);  // the output stays indexed from value_begin
-      value_begin = a;
-      value_end = b;
-    } else if (split_k != 0 || lo < hi) {
-      return;  // nothing of this segment is mine
-    }
-    // (a segment with no values in range: share 0 walks it whole for its checks)
-  }
   if (seg_start >= seg_end) {
     if (tid == 0 && v_next != ~0ull && v_next != vi && seg_start < src_len) report(err, vi, kErrBadSegment);
     if (tid == 0 && v_next == ~0ull) report(err, vi, kErrBadRead);  // no stream left for the requested values
@@ -2088,16 +2067,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       }
       __syncthreads();  // s_flags is rewritten by the next round
     }
-  } else if (p_split <= 1) {
-    run_segment(blockIdx.x, false, 0, 0);
   } else {
-    // the shares of one segment run on one XCD (workgroup ids congruent mod
-    // 8) so the walks re-reading its first windows hit the same L2
-    const uint32_t x = blockIdx.x & 7u, y = blockIdx.x >> 3;
-    split_n = p_split;
-    split_k = y % p_split;
-    const uint64_t gg = (uint64_t)(y / p_split) * 8u + x;
-    if (gg < p_nsegs) run_segment(gg, false, 0, 0);
+    // (one call site per instance: a second one makes the compiler outline
+    // run_segment into a call with a ~700-byte stack frame)
+    run_segment(blockIdx.x, false, 0, 0);
   }
 }
 
@@ -2165,7 +2138,7 @@ static int default_variant(uint64_t src_len, uint64_t est_values) {
 static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode, uint64_t rows_per_group,
                         uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes, const RleJob* jobs_d,
-                        uint32_t njobs_d, uint32_t split = 1, const uint64_t* dcount = nullptr) {
+                        uint32_t njobs_d, const uint64_t* dcount = nullptr) {
   if (nsegs == 0 || nvalues == 0) return ORCG_OK;
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   if (dst_bytes != 8 && dst_bytes != 4 && dst_bytes != 2)
@@ -2184,15 +2157,11 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     ctx->num_cus = cus;
   }
   const unsigned drain = (unsigned)std::min<uint64_t>(nsegs, 6ull * (uint64_t)ctx->num_cus);
-  // split launches: nsegs x split workgroups (whole groups of 8 segments,
-  // see the kernel's XCD mapping); the queueing instances never split
-  uint32_t sp = 1;
-  const unsigned grid_n = split > 1 ? (unsigned)(((nsegs + 7) / 8) * 8 * split) : (unsigned)nsegs;
 
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
   hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
                      d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
-                     ctx->d_err, dq, dpar, jobs_d, njobs_d, sp, dcount)
+                     ctx->d_err, dq, dpar, jobs_d, njobs_d, dcount)
 // single-stream instances (+ the multi-stream one for the default's
 // instances, ORCG_KX; the tuning variants have none, ORCG_KX1)
 #define ORCG_KX1(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                 \
@@ -2247,8 +2216,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     ORCG_KX(DO, 8, false, 6, 2, 2, drain);                                           \
   } while (0)
 
-  if (split > 1 && variant != 3 && variant != 7 && variant != 26) sp = split;
-  const unsigned grid_s = sp > 1 ? grid_n : (unsigned)nsegs;
+  const unsigned grid_s = (unsigned)nsegs;
   switch (variant) {
     case 2: ORCG_KX(kWide | kOptD3, 33, false, 1, 0, 0, grid_s); break;  // 33 KB register-filled serial, no queue
     case 3: ORCG_DEFERRING(kSer | kOptD3, 21, 6, kSer | kOptD3); break;   // 21 KB serial + dense drain
@@ -2297,42 +2265,14 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
   return hip_check(ctx, hipGetLastError(), "rlev2_tiled_kernel launch");
 }
 
-// Split factor of a launch whose segments are too few to fill the GPU
-// (~2,048 workgroups: 256 CUs x 8): segments of >= 8,192 values are split in
-// 2, 4 or 8 shares of >= 4,096 values each. ORCG_SPLIT=k forces k (1 = off).
-static uint32_t auto_split(uint64_t nsegs, uint64_t values) {
-  static const int forced = [] {
-    const char* e = getenv("ORCG_SPLIT");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced > 0) return (uint32_t)std::min(forced, 8);
-  // off by default: a split workgroup walks every run before its share, and
-  // the serial walk (~2 us per run on a lone workgroup) is the critical path
-  // of the long-run segments this was meant for (C5 child streams: 4.9 ->
-  // 8.1 ms device decode with split 8)
-  if (forced == 0) return 1;
-  if (nsegs == 0) return 1;
-  const uint64_t per = values / nsegs;
-  uint32_t s = 1;
-  while (s < 8 && nsegs * s < 2048 && per / (2 * s) >= 4096) s *= 2;
-  return s;
-}
-
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
-                       int dst_bytes, uint32_t split, const uint64_t* d_count) {
+                       int dst_bytes, const uint64_t* d_count) {
   int variant = ctx->rlev2_variant;
-  const uint64_t est = positions_mode ? nsegs * rows_per_group : nvalues;
-  if (split == 0) split = auto_split(nsegs, est);
-  if (variant == 0) {
-    variant = default_variant(src_len, est);
-    // split launches take the queue-less instances: the 33 KB serial one for
-    // wide values, else the union instance (it routes each window by its runs)
-    if (split > 1 && variant == 3) variant = 6;
-  }
+  if (variant == 0) variant = default_variant(src_len, positions_mode ? nsegs * rows_per_group : nvalues);
   return launch_tiled(ctx, variant, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode, rows_per_group,
-                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, split, d_count);
+                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count);
 }
 
 // Job tables go through a pinned ring mirrored on the device: entries are
