@@ -202,6 +202,12 @@ int orcg_row_reader_seek_to_row(orcg_row_reader* rr, uint64_t row);
  * next / seek); the reader's orcg_reader_last_error also carries it, but is
  * shared with every row reader of that reader */
 const char* orcg_row_reader_last_error(const orcg_row_reader* rr);
+// Seconds this row reader spent so far: out6[0] host preparation (decompression)
+// inside a stripe's decode job, [1] upload + GPU decode, [2] D2H into the
+// pinned slab, [3] slab allocation, [4] look-ahead preparation of the next
+// stripe (worker thread); [5] the caller's waits for a stripe's slab in
+// next() / seekToRow(). Diagnostics; no reference counterpart.
+int orcg_row_reader_timings(orcg_row_reader* rr, double* out6);
 /* the last batch's view of column type_id (host pointers, see above) */
 int orcg_row_reader_column(const orcg_row_reader* rr, uint32_t type_id, orcg_column_view* view, uint64_t* begin,
                            uint64_t* count);

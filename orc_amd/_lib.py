@@ -186,6 +186,7 @@ SIGNATURES += [
     ("orcg_host_alloc", [u64], vp),
     ("orcg_host_free", [vp], None),
     ("orcg_row_reader_last_error", [vp], cp),
+    ("orcg_row_reader_timings", [vp, ctypes.POINTER(ctypes.c_double)], i32),
     ("orcg_row_reader_seek_to_row", [vp, u64], i32),
     ("orcg_row_reader_column", [vp, u32, ctypes.POINTER(ColumnView), ctypes.POINTER(u64), ctypes.POINTER(u64)],
      i32),

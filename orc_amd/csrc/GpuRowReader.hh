@@ -35,6 +35,7 @@
 #pragma once
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
@@ -439,9 +440,22 @@ class RowReader {
   void seekToRow(uint64_t rowNumber);
   // RowReader::getSelectedColumns()[id]
   bool isSelected(uint32_t id) const { return orcg_row_reader_is_selected(rr_, id) != 0; }
+  // diagnostics (no reference counterpart): with profiling on, seconds spent
+  // in next() on [0] the row reader's C call (waits for a stripe's slab
+  // included), [1] fill (views, per-row work), [2] the bulk copies; [3..8]
+  // the row reader's own counters (orcg_row_reader_timings)
+  void setProfiling(bool on) { prof_on_ = on; }
+  std::vector<double> getProfile() const {
+    std::vector<double> p(prof_, prof_ + 3);
+    double w[6];
+    if (orcg_row_reader_timings(rr_, w) == ORCG_OK) p.insert(p.end(), w, w + 6);
+    return p;
+  }
 
  private:
   void fill(uint32_t id, ColumnVectorBatch& b);
+  bool prof_on_ = false;
+  double prof_[3] = {0, 0, 0};
   Reader& r_;
   orcg_row_reader* rr_ = nullptr;
   bool lazy_ = false;
@@ -649,12 +663,23 @@ inline std::unique_ptr<ColumnVectorBatch> RowReader::createRowBatch(uint64_t cap
 
 inline bool RowReader::next(ColumnVectorBatch& batch) {
   uint64_t rows = 0;
+  using clk = std::chrono::steady_clock;
+  clk::time_point t0, t1, t2;
+  if (prof_on_) t0 = clk::now();
   r_.check(orcg_row_reader_next(rr_, batch.capacity, &rows));
   batch.numElements = rows;
   if (rows == 0) return false;
+  if (prof_on_) t1 = clk::now();
   copies_.clear();
   fill(0, batch);
+  if (prof_on_) t2 = clk::now();
   pool_->run(copies_);
+  if (prof_on_) {
+    const clk::time_point t3 = clk::now();
+    prof_[0] += std::chrono::duration<double>(t1 - t0).count();
+    prof_[1] += std::chrono::duration<double>(t2 - t1).count();
+    prof_[2] += std::chrono::duration<double>(t3 - t2).count();
+  }
   return true;
 }
 

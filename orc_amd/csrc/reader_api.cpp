@@ -1633,6 +1633,12 @@ struct orcg_row_reader {
   std::string last_error;  // this row reader's last failure (orcg_row_reader_last_error)
   std::deque<uint64_t> jobs;
   bool stop = false;
+  // worker seconds: [0] prepare inside a job (host decompression the
+  // look-ahead did not do), [1] upload + decode, [2] D2H into the slab,
+  // [3] slab (re)allocation, [4] look-ahead prepare; [5] caller waits for a
+  // slab (orcg_row_reader_timings)
+  std::atomic<uint64_t> prof[6] = {};  // nanoseconds
+  void addp(int i, double sec) { prof[i].fetch_add((uint64_t)(sec * 1e9), std::memory_order_relaxed); }
   // the worker's own context (stream, error record, scratch, queues): the
   // caller's context may be driven by its thread while the worker decodes
   // ahead, e.g. by another reader sharing it
@@ -1675,6 +1681,7 @@ struct orcg_row_reader {
     uint64_t total = 0;
     for (auto& bb : bufs) total += (bb.second.second + 255) & ~(uint64_t)255;
     if (total > sl.cap) {
+      const double ta = now_s();
       if (sl.h) (void)hipHostFree(sl.h);
       sl.h = nullptr;
       sl.cap = 0;
@@ -1682,6 +1689,7 @@ struct orcg_row_reader {
       if (hipHostMalloc((void**)&sl.h, ncap, hipHostMallocDefault) != hipSuccess)
         return r->fail(ORCG_OUT_OF_MEMORY, "pinned row batch allocation failed");
       sl.cap = ncap;
+      addp(3, now_s() - ta);
     }
     uint64_t w = 0;
     for (auto& bb : bufs) {
@@ -1702,6 +1710,7 @@ struct orcg_row_reader {
     HostStage& hs = stage[t & 1];
     int rc;
     std::string err;
+    const double t0 = now_s();
     {
       std::lock_guard<std::mutex> lk(r->mu);
       orcg_reader::Active act(r, own, selected, lazy_dict);
@@ -1714,11 +1723,16 @@ struct orcg_row_reader {
         rc = hs.rc;
       }
       if (rc) err = hs.err;
+      const double t1 = now_s();
       if (!rc) {
         rc = r->upload_and_decode(hs, *dev);
+        const double t2 = now_s();
         if (!rc) rc = copy_out(sl);
         if (rc) err = r->last_error;
+        addp(1, t2 - t1);
+        addp(2, now_s() - t2);
       }
+      addp(0, t1 - t0);
       prepared[t & 1] = ~0ull;  // the stage is reused by stripe t + 2
     }
     {
@@ -1738,10 +1752,12 @@ struct orcg_row_reader {
         idle = jobs.empty() && !stop;
       }
       if (idle) {
+        const double tp = now_s();
         std::lock_guard<std::mutex> lk(r->mu);
         orcg_reader::Active act(r, own, selected, lazy_dict);
         prepared[u & 1] = u;
         (void)r->prepare(u, stage[u & 1]);  // a failure is kept in the stage
+        addp(4, now_s() - tp);
       }
     }
   }
@@ -1777,7 +1793,9 @@ struct orcg_row_reader {
     HostSlab& sl = slab[s & 1];
     const bool mine = (slab_state[s & 1] == 2 && sl.stripe == s) || (slab_state[s & 1] == 1 && slab_want[s & 1] == s);
     if (!mine) post(lk, s);
+    const double tw = now_s();
     cv.wait(lk, [&] { return slab_state[s & 1] == 2; });
+    addp(5, now_s() - tw);
     if (sl.rc) {
       const int rc = sl.rc;
       last_error = sl.err;
@@ -2155,6 +2173,12 @@ int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows)
     rr->row_in_stripe = 0;
   }
   *rows = n;
+  return ORCG_OK;
+}
+
+int orcg_row_reader_timings(orcg_row_reader* rr, double* out6) {
+  if (!rr || !out6) return ORCG_INVALID_ARGUMENT;
+  for (int i = 0; i < 6; ++i) out6[i] = rr->prof[i].load(std::memory_order_relaxed) * 1e-9;
   return ORCG_OK;
 }
 

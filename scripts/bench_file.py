@@ -130,13 +130,14 @@ def row_reader_leg(path, nrows, stripes_wall):
                                exe, "-L" + os.path.join(ROOT, "orc_amd"), "-lorcgpu",
                                "-Wl,-rpath," + os.path.join(ROOT, "orc_amd"), "-Wl,-rpath,/opt/rocm/lib"])
     out = {}
-    for cap in (1024, 16384):
-        r = subprocess.run([exe, path, "--bench", "--batch", str(cap)], capture_output=True, text=True, timeout=600)
+    for cap, extra in ((1024, []), (16384, []), (1024, ["--pinned"])):
+        r = subprocess.run([exe, path, "--bench", "--batch", str(cap)] + extra, capture_output=True, text=True,
+                           timeout=600)
         if r.returncode != 0:
             raise SystemExit("row reader bench failed: %s" % r.stderr[-500:])
         d = json.loads(r.stdout.strip().splitlines()[-1])
         d["vs_read_stripes_wall"] = round(d["seconds"] / max(stripes_wall, 1e-9), 2)
-        out["batch_%d" % cap] = d
+        out["batch_%d%s" % (cap, "_pinned_pool" if extra else "")] = d
     return out
 
 

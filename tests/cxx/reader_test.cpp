@@ -264,8 +264,10 @@ int main(int argc, char** argv) {
     PinnedMemoryPool pinned_pool;
     ReaderOptions ropts;
     if (pinned) ropts.setMemoryPool(pinned_pool);
+    const auto tc = std::chrono::steady_clock::now();
     Reader reader(ctx, argv[1], ropts);
     auto rows = reader.createRowReader(opts);
+    rows->setProfiling(bench);
     g_rows = rows.get();
     g_names.assign(orcg_reader_num_types(reader.get()), {});
     names_of(reader, 0, g_names);
@@ -290,9 +292,17 @@ int main(int argc, char** argv) {
         n += batch->numElements;
         ++batches;
       }
-      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      printf("{\"rows\": %llu, \"batches\": %llu, \"seconds\": %.6f, \"mrows_per_s\": %.3f}\n",
-             (unsigned long long)n, (unsigned long long)batches, s, n / s / 1e6);
+      const auto t1 = std::chrono::steady_clock::now();
+      const double s = std::chrono::duration<double>(t1 - t0).count();
+      const double sc = std::chrono::duration<double>(t1 - tc).count();
+      const std::vector<double> p = rows->getProfile();
+      printf("{\"rows\": %llu, \"batches\": %llu, \"seconds\": %.6f, \"mrows_per_s\": %.3f, "
+             "\"seconds_from_open\": %.6f, \"profile_s\": {\"c_next\": %.4f, \"fill\": %.4f, \"copies\": %.4f, "
+             "\"worker_prepare\": %.4f, \"worker_decode\": %.4f, \"worker_d2h\": %.4f, \"worker_slab_alloc\": %.4f, "
+             "\"worker_lookahead\": %.4f, \"caller_wait\": %.4f}}\n",
+             (unsigned long long)n, (unsigned long long)batches, s, n / s / 1e6, sc, p[0], p[1], p[2],
+             p.size() > 3 ? p[3] : 0., p.size() > 4 ? p[4] : 0., p.size() > 5 ? p[5] : 0., p.size() > 6 ? p[6] : 0.,
+             p.size() > 7 ? p[7] : 0., p.size() > 8 ? p[8] : 0.);
       return n == reader.getNumberOfRows() || ranged ? 0 : 1;
     }
     uint64_t total = 0;
