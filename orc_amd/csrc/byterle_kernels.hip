@@ -12,7 +12,7 @@
 // group starts + the longest group's tail, one coalesced 16-B load per
 // thread); the window's group starts are found in parallel (chunk exits,
 // block hops, a workgroup scan: byterle_kernel below) and the decoded bytes
-// pass through an LDS stage to coalesced stores.
+// are assembled a dword per lane through an owner map, stored coalesced.
 // In boolean mode every decoded byte becomes 8 output rows (chars 0/1).
 #include "rlev2_device.hh"
 
@@ -110,8 +110,10 @@ __device__ __forceinline__ uint32_t group_dec(uint32_t h) { return h < 0x80 ? h 
 //      (<= 7 hops) and walks the groups starting in its chunk (<= 8);
 //   5. a workgroup scan of the groups' decoded bytes gives each group its
 //      first decoded index;
-//   6. the groups' decoded bytes go through an LDS stage (16 KB at a time)
-//      and leave it with coalesced stores.
+//   6. the groups go to a table and an owner map (a scatter of group
+//      indices at their first whole dword, then a prefix max); each thread
+//      assembles dwords of decoded bytes from the groups the map names and
+//      stores them straight out, consecutive dwords on consecutive lanes.
 // Errors are reported per group with atomicMin on (decoded index, code), so
 // the earliest in stream order wins, as the reference's serial loop raises
 // it (ByteRleDecoderImpl::nextInternal, :449-505).
@@ -131,6 +133,10 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
   __shared__ uint16_t s_bentry[kBBlocks + 1];
   __shared__ uint32_t s_wsum[2][kBThreads / kWave];
   __shared__ uint32_t s_ctl[4];  // next window position, -, error seen
+  // the window's groups: stream position, first decoded byte (step 6)
+  __shared__ uint16_t s_gpos[kBChunk / 2 + 1];
+  __shared__ uint32_t s_gdec[kBChunk / 2 + 1];
+  __shared__ uint32_t s_wmax[kBThreads / kWave];
   uint16_t* s_exit2 = s_exit + kBChunk;
   const uint8_t* s_bytes = (const uint8_t*)s_win;
   const uint64_t g = blockIdx.x;
@@ -263,9 +269,8 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
     }
     const uint32_t np = s_ctl[0];
     // 5b. my groups in stream order: the errors (the serial loop's checks, at
-    // each group's decoded index; atomicMin keeps the earliest) and how many
-    // of them are decoded (none past an error or past the bytes needed)
-    uint32_t nvalid = 0;
+    // each group's decoded index; atomicMin keeps the earliest), none past
+    // the bytes needed
     if (qs != kBNone) {
       uint32_t p = qs, d = dec_base;
       while (p < cs + 16 && p < lim) {
@@ -278,7 +283,6 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
           s_ctl[2] = 1;
           break;
         }
-        ++nvalid;
         if ((uint64_t)p + gl > seg_left) {  // the group runs past the segment
           report(err, di + L, kErrBadSegment);
           s_ctl[2] = 1;
@@ -288,39 +292,117 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
         d += L;
       }
     }
-    // 6. expansion through an LDS stage of decoded bytes (s_exit's 16 KB,
-    // dead now), one stage-full at a time: each thread copies its groups'
-    // bytes in (runs as word fills), then the workgroup writes the stage out
-    // with consecutive lanes on consecutive output (coalesced stores; a
-    // thread storing its own groups scatters every store over 64 lines)
-    uint8_t* s_stage = (uint8_t*)s_exit;
-    constexpr uint32_t kStage = 2 * kBChunk * sizeof(uint16_t);
-    for (uint32_t sb = 0; sb < dec_total; sb += kStage) {
+    // 6. the window's decoded bytes straight to the output, one dword of them
+    // (4 bytes, 32 rows) per thread per step, consecutive dwords on
+    // consecutive lanes. A dword's bytes come from the last group starting at
+    // or before its first byte (and the groups after it): the groups go to a
+    // table (stream position, first decoded byte), each scatters its index
+    // into an owner map at its first whole dword, and a prefix max fills the
+    // map, 4096 dwords (16 KB of decoded bytes) per round.
+    uint32_t ng_base = ng_inc - ng;
+#pragma unroll
+    for (int w = 0; w < kBThreads / kWave; ++w) ng_base += w < wave ? s_wsum[0][w] : 0u;
+    if (qs != kBNone) {
       uint32_t p = qs, d = dec_base;
-      for (uint32_t k = 0; k < nvalid && d < sb + kStage; ++k) {
+      for (uint32_t k = 0; k < ng; ++k) {
+        s_gpos[ng_base + k] = (uint16_t)p;
+        s_gdec[ng_base + k] = d;
         const uint32_t h = chunk_byte(mine, p - cs);
-        const uint32_t L = group_dec(h);
-        const uint32_t a = d > sb ? d : sb, b = d + L < sb + kStage ? d + L : sb + kStage;
-        if (a < b) {
-          uint32_t x = a - sb;
-          const uint32_t xe = b - sb;
-          if (h < 0x80) {
-            const uint32_t v = s_bytes[p + 1];
-            for (; x < xe && (x & 3u); ++x) s_stage[x] = (uint8_t)v;
-            for (; x + 4 <= xe; x += 4) *(uint32_t*)(s_stage + x) = v * 0x01010101u;
-            for (; x < xe; ++x) s_stage[x] = (uint8_t)v;
-          } else {
-            const uint8_t* lit = s_bytes + p + 1 + (a - d);
-            for (uint32_t y = 0; x < xe; ++x, ++y) s_stage[x] = lit[y];
-          }
-        }
         p += group_len(h);
-        d += L;
+        d += group_dec(h);
+      }
+    }
+    uint32_t* s_own = (uint32_t*)s_exit;  // s_exit's 16 KB, dead now
+    constexpr uint32_t kRound = 2 * kBChunk * sizeof(uint16_t) / 4;  // dwords per round
+    for (uint32_t sb = 0; sb < dec_total; sb += 4 * kRound) {
+      for (uint32_t k = (uint32_t)tid; k < kRound; k += kBThreads) s_own[k] = 0;
+      __syncthreads();
+      if (qs != kBNone) {
+        uint32_t d = dec_base;
+        for (uint32_t k = 0; k < ng; ++k) {
+          const uint32_t slot = d <= sb ? 0u : (d - sb + 3u) >> 2;
+          if (slot < kRound) atomicMax(&s_own[slot], ng_base + k);
+          d += group_dec(chunk_byte(mine, s_gpos[ng_base + k] - cs));
+        }
       }
       __syncthreads();
-      const uint32_t n = dec_total - sb < kStage ? dec_total - sb : kStage;
-      for (uint32_t k = (uint32_t)tid; k < n; k += kBThreads) emit<kBool>(dst, vi + sb + k, s_stage[k], begin, end, ones);
+      {
+        // prefix max: thread t holds slots [16t, 16t + 16)
+        bu4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = *(const bu4*)(s_own + 16 * tid + 4 * k);
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          m = max(m, v[k].x); v[k].x = m;
+          m = max(m, v[k].y); v[k].y = m;
+          m = max(m, v[k].z); v[k].z = m;
+          m = max(m, v[k].w); v[k].w = m;
+        }
+        uint32_t inc = m;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) {
+          const uint32_t u = (uint32_t)__shfl_up((int)inc, o);
+          if (lane >= o) inc = max(inc, u);
+        }
+        if (lane == kWave - 1) s_wmax[wave] = inc;
+        uint32_t before = (uint32_t)__shfl_up((int)inc, 1);
+        if (lane == 0) before = 0;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < kBThreads / kWave; ++w)
+          if (w < wave) before = max(before, s_wmax[w]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k].x = max(v[k].x, before);
+          v[k].y = max(v[k].y, before);
+          v[k].z = max(v[k].z, before);
+          v[k].w = max(v[k].w, before);
+          *(bu4*)(s_own + 16 * tid + 4 * k) = v[k];
+        }
+      }
       __syncthreads();
+      const uint32_t left = dec_total - sb;
+      const uint32_t nd = left >= 4 * kRound ? kRound : (left + 3u) >> 2;
+      for (uint32_t j = (uint32_t)tid; j < nd; j += kBThreads) {
+        const uint32_t x0 = sb + 4u * j;  // decoded offset of the dword in the window
+        uint32_t g = s_own[j];
+        uint32_t d = s_gdec[g], p = s_gpos[g], h = s_bytes[p];
+        uint32_t gend = d + group_dec(h);
+        uint32_t w4;
+        if (gend >= x0 + 4u) {
+          if (h < 0x80) {
+            w4 = (uint32_t)s_bytes[p + 1] * 0x01010101u;
+          } else {
+            const uint32_t so = p + 1u + (x0 - d);
+            const uint32_t* w = s_win + (so >> 2);
+            w4 = __builtin_amdgcn_alignbyte(w[1], w[0], so & 3u);
+          }
+        } else {
+          w4 = 0;
+          for (uint32_t b = 0; b < 4 && x0 + b < dec_total; ++b) {
+            while (x0 + b >= gend) {
+              ++g;
+              d = s_gdec[g];
+              p = s_gpos[g];
+              h = s_bytes[p];
+              gend = d + group_dec(h);
+            }
+            const uint32_t y = h < 0x80 ? s_bytes[p + 1] : s_bytes[p + 1u + (x0 + b - d)];
+            w4 |= y << (8 * b);
+          }
+        }
+        const uint64_t i = vi + x0;
+        const uint32_t nb = dec_total - x0 < 4u ? dec_total - x0 : 4u;
+        if constexpr (!kBool) {
+          if (nb == 4 && i >= begin && i + 4 <= end && ((uintptr_t)(dst + (i - begin)) & 3u) == 0) {
+            *(uint32_t*)(dst + (i - begin)) = w4;
+            continue;
+          }
+        }
+        for (uint32_t b = 0; b < nb; ++b) emit<kBool>(dst, i + b, (w4 >> (8 * b)) & 0xffu, begin, end, ones);
+      }
+      __syncthreads();  // the map is rebuilt by the next round
     }
     const bool stop = s_ctl[2] != 0;
     __syncthreads();  // the window and the tables are rewritten by the next pass

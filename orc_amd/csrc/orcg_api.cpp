@@ -4,7 +4,12 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <sys/mman.h>
+
 #include <algorithm>
+#include <mutex>
+#include <thread>
+#include <unordered_map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -137,6 +142,103 @@ uint32_t parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_l
 }
 
 }  // namespace
+// Page-locked host memory. Large buffers (the reader's staging, the row
+// reader's slabs) are anonymous mappings advised to transparent huge pages,
+// faulted in by several threads and then registered with HIP: measured on the
+// MI355X hosts (scripts/probes/pin_probe.cpp), 256 MB costs ~15 ms to fault +
+// 0.5 ms to register this way against ~48 ms for hipHostMalloc (4 KB pages
+// pinned one by one), at the same D2H rate (57 GB/s). Small buffers, or a
+// failed registration, use hipHostMalloc.
+namespace {
+std::mutex g_pin_mu;
+std::unordered_map<void*, size_t> g_pin_maps;  // registered mappings -> length
+constexpr size_t kHuge = size_t(2) << 20;
+}  // namespace
+
+void* pinned_alloc(size_t bytes) {
+  if (bytes == 0) bytes = 1;
+  if (bytes >= (size_t(8) << 20)) {
+    const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
+    void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m != MAP_FAILED) {
+      (void)madvise(m, len, MADV_HUGEPAGE);
+      // fault the pages in on a few threads (one write per 4 KB page: a huge
+      // page faults whole on its first write, a small one each)
+      const size_t pages = len >> 12;
+      const unsigned nt = (unsigned)std::min<size_t>(8, std::max<size_t>(1, len / (size_t(32) << 20)));
+      std::vector<std::thread> ts;
+      for (unsigned t = 0; t < nt; ++t)
+        ts.emplace_back([=] {
+          volatile char* b = (volatile char*)m;
+          for (size_t pg = pages * t / nt; pg < pages * (t + 1) / nt; ++pg) b[pg << 12] = 0;
+        });
+      for (auto& th : ts) th.join();
+      if (hipHostRegister(m, len, hipHostRegisterDefault) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        g_pin_maps[m] = len;
+        return m;
+      }
+      (void)hipGetLastError();
+      munmap(m, len);
+    }
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void pinned_free(void* p) {
+  if (!p) return;
+  size_t len = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_maps.find(p);
+    if (it != g_pin_maps.end()) {
+      len = it->second;
+      g_pin_maps.erase(it);
+    }
+  }
+  if (len) {
+    (void)hipHostUnregister(p);
+    munmap(p, len);
+  } else {
+    (void)hipHostFree(p);
+  }
+}
+
+unsigned side_lanes() {
+  static const unsigned n = [] {
+    const char* e = getenv("ORCG_LANES");
+    const int v = e ? atoi(e) : 4;
+    return (unsigned)std::max(1, std::min(v, 16));
+  }();
+  return n;
+}
+
+Ctx* ctx_lane(Ctx* base, size_t k) {
+  if (!base->ev_fork && hipEventCreateWithFlags(&base->ev_fork, hipEventDisableTiming) != hipSuccess) {
+    base->ev_fork = nullptr;
+    return nullptr;
+  }
+  while (base->lanes.size() <= k) {
+    orcg_ctx* l = nullptr;
+    hipEvent_t e = nullptr;
+    if (orcg_ctx_create(base->device, &l) != ORCG_OK) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      orcg_ctx_destroy(l);
+      return nullptr;
+    }
+    base->lanes.push_back(l);
+    base->ev_join.push_back(e);
+  }
+  Ctx* l = base->lanes[k];
+  l->rlev2_variant = base->rlev2_variant;
+  if (!l->num_cus) l->num_cus = base->num_cus;
+  return l;
+}
 }  // namespace orcg
 
 using namespace orcg;
@@ -209,22 +311,17 @@ int orcg_ctx_create(int device, orcg_ctx** out) {
   return ORCG_OK;
 }
 
-void* orcg_host_alloc(uint64_t bytes) {
-  void* p = nullptr;
-  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  return p;
-}
+void* orcg_host_alloc(uint64_t bytes) { return orcg::pinned_alloc(bytes); }
 
-void orcg_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
-}
+void orcg_host_free(void* p) { orcg::pinned_free(p); }
 
 void orcg_ctx_destroy(orcg_ctx* c) {
   if (!c) return;
   hipSetDevice(c->device);
+  for (Ctx* l : c->lanes) orcg_ctx_destroy(static_cast<orcg_ctx*>(l));
+  if (c->ev_fork) hipEventDestroy(c->ev_fork);
+  for (hipEvent_t e : c->ev_join)
+    if (e) hipEventDestroy(e);
   if (c->stream) hipStreamSynchronize(c->stream);
   for (int i = 0; i < 8; ++i)
     if (c->d_scratch[i]) hipFree(c->d_scratch[i]);

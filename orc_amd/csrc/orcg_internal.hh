@@ -58,7 +58,19 @@ struct Ctx {
   void* h_jobs = nullptr;
   void* d_jobs = nullptr;
   uint64_t jobs_cap = 0, jobs_used = 0;
+  // side contexts (own stream, scratch, queues) the file reader decodes
+  // sibling column subtrees on concurrently, forked from and joined back into
+  // this context's stream with events; created on first use (ctx_lane)
+  std::vector<Ctx*> lanes;
+  hipEvent_t ev_fork = nullptr;
+  std::vector<hipEvent_t> ev_join;
 };
+
+// Side context k of `base` (created on first use, settings copied from base);
+// nullptr if it cannot be created.
+Ctx* ctx_lane(Ctx* base, size_t k);
+// Side streams the file reader may use (ORCG_LANES, default 4; 1 = none).
+unsigned side_lanes();
 
 // One RLEv2 stream of a multi-stream launch: its bytes, segments, output
 // (int64) and value count; seg_base = the launch-wide index of its first
@@ -84,6 +96,10 @@ struct RleJob {
 };
 
 int set_error(Ctx* ctx, int status, const std::string& msg);
+// page-locked host memory (transparent huge pages + hipHostRegister for large
+// buffers, hipHostMalloc otherwise); pinned_free takes either kind
+void* pinned_alloc(size_t bytes);
+void pinned_free(void* p);
 int hip_check(Ctx* ctx, hipError_t e, const char* what);
 int scratch(Ctx* ctx, int slot, size_t bytes, void** out);
 // Wait for the context stream and fold the device error record into a status.

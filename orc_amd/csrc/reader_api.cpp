@@ -17,6 +17,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <chrono>
@@ -208,17 +209,15 @@ struct HostStage {
   uint64_t ngroups = 0;    // row groups with row-index positions (0: host plans only)
   uint64_t n_pos = 0, n_plan = 0;  // RLE streams cut by the row index / by a host plan
   uint64_t rows_off = 0;   // staging offset of int64 rows[g] = g * stride
-  ~HostStage() {
-    if (h) (void)hipHostFree(h);
-  }
+  ~HostStage() { pinned_free(h); }
   bool ensure(uint64_t bytes, uint64_t keep) {
     if (bytes <= cap) return true;
     const uint64_t ncap = std::max<uint64_t>(bytes + (bytes >> 2), 1 << 20);
-    uint8_t* nh = nullptr;
-    if (hipHostMalloc((void**)&nh, ncap, hipHostMallocDefault) != hipSuccess) return false;
+    uint8_t* nh = (uint8_t*)pinned_alloc(ncap);
+    if (!nh) return false;
     if (h) {
       if (keep) memcpy(nh, h, keep);
-      (void)hipHostFree(h);
+      pinned_free(h);
     }
     h = nh;
     cap = ncap;
@@ -394,6 +393,46 @@ struct orcg_reader {
   // not read back mid-stripe (one stream synchronisation per nullable column
   // saved); has_nulls is settled with the stripe's checks.
   bool device_counts(const Col& c) const;
+  // Side streams for sibling subtrees (ORCG_LANES, default 4; 1 = one
+  // stream). in_lane: decode() runs on a side context (no nested forks).
+  bool in_lane = false;
+  // A list / map decoded under a fork whose children wait for its element
+  // count (offsets[n] on the device), decoded on the same side context.
+  struct Pending {
+    uint32_t id;
+    const int64_t* d_total;
+    int64_t* child_rows;
+    Ctx* lane;
+  };
+  std::vector<Pending>* pending = nullptr;
+  // read_back over several side contexts: the D2H copies on each one's
+  // stream, then one synchronisation per stream used
+  int read_back_lanes(const std::vector<Pending>& ps, uint64_t* out) {
+    if (ps.size() > sync_cap) {
+      if (h_sync) (void)hipHostFree(h_sync);
+      h_sync = nullptr;
+      sync_cap = 0;
+      const size_t cap = std::max<size_t>(64, ps.size());
+      if (hipHostMalloc((void**)&h_sync, cap * 8, hipHostMallocDefault) != hipSuccess)
+        return fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed");
+      sync_cap = cap;
+    }
+    std::vector<Ctx*> lanes_used;
+    for (size_t i = 0; i < ps.size(); ++i) {
+      const int rc = hip_check(ps[i].lane, hipMemcpyAsync(h_sync + i, ps[i].d_total, 8, hipMemcpyDeviceToHost,
+                                                          ps[i].lane->stream), "D2H");
+      if (rc) return fail(rc, ps[i].lane->last_error);
+      if (std::find(lanes_used.begin(), lanes_used.end(), ps[i].lane) == lanes_used.end())
+        lanes_used.push_back(ps[i].lane);
+    }
+    for (Ctx* l : lanes_used) {
+      const int rc = hip_check(l, hipStreamSynchronize(l->stream), "hipStreamSynchronize");
+      if (rc) return fail(rc, l->last_error);
+    }
+    for (size_t i = 0; i < ps.size(); ++i) out[i] = h_sync[i];
+    return ORCG_OK;
+  }
+  static unsigned num_lanes() { return side_lanes(); }
   // row-group context of the column being decoded (segments())
   const int64_t* cur_rows = nullptr;  // device: first row of each row group, in the column's rows
   uint64_t cur_n = 0;
@@ -972,19 +1011,106 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     ORCG_ALLOC(int64_t, off, n + 1);
     if ((rc = launch_exclusive_scan(ctx, rlen, n, off))) return fail_ctx(rc);
     c.offsets = off;
-    uint64_t total = 0;
-    if ((rc = read_back({off + n}, &total))) return rc;
     // the children's row groups start at the list offsets of the parent's
     int64_t* child_rows = nullptr;
     if (rg_rows && H->ngroups) {
       ORCG_ALLOC_TO(int64_t, child_rows, H->ngroups);
       if ((rc = launch_rg_child_rows(ctx, off, rg_rows, H->ngroups, child_rows))) return fail_ctx(rc);
     }
+    if (pending) {
+      // under a fork: the children wait for the fork's next level, whose
+      // element counts are read back together (one synchronisation per level
+      // instead of one per list / map, which would stall the other lanes)
+      pending->push_back(Pending{id, off + n, child_rows, ctx});
+      return ORCG_OK;
+    }
+    uint64_t total = 0;
+    if ((rc = read_back({off + n}, &total))) return rc;
     for (uint32_t st : footer.types[id].subtypes)
       if ((rc = decode(st, total, nullptr, total, child_rows))) return rc;
   } else if (k == ORCG_TYPE_STRUCT) {
+    std::vector<uint32_t> kids;
     for (uint32_t st : footer.types[id].subtypes)
-      if ((rc = decode(st, n, c.nn, nonnull, rg_rows, c.nn ? d_nonnull : nullptr, &c))) return rc;
+      if (selected[st] && H->cols[st].supported) kids.push_back(st);
+    const unsigned nl = in_lane ? 1u : (unsigned)std::min<size_t>(num_lanes(), kids.size());
+    if (nl <= 1) {
+      for (uint32_t st : kids)
+        if ((rc = decode(st, n, c.nn, nonnull, rg_rows, c.nn ? d_nonnull : nullptr, &c))) return rc;
+    } else {
+      // sibling subtrees on side streams (their kernels run concurrently:
+      // most launches of a stripe are one workgroup per row group, a
+      // fraction of the chip), forked after this column's work and joined
+      // back before anything reads their outputs
+      Ctx* base = ctx;
+      if (!ctx_lane(base, 0)) return fail(ORCG_DEVICE_ERROR, "side stream creation failed");
+      if ((rc = hip_check(ctx, hipEventRecord(base->ev_fork, base->stream), "fork event"))) return fail_ctx(rc);
+      std::vector<uint8_t> used(nl, 0);
+      std::vector<Pending> level;  // lists / maps whose children wait for their element counts
+      pending = &level;
+      for (size_t j = 0; j < kids.size() && !rc; ++j) {
+        Ctx* L = ctx_lane(base, j % nl);
+        if (!L) {
+          rc = fail(ORCG_DEVICE_ERROR, "side stream creation failed");
+          break;
+        }
+        if (!used[j % nl]) {
+          used[j % nl] = 1;
+          if ((rc = hip_check(base, hipStreamWaitEvent(L->stream, base->ev_fork, 0), "fork wait"))) {
+            rc = fail_ctx(rc);
+            break;
+          }
+        }
+        ctx = L;
+        in_lane = true;
+        rc = decode(kids[j], n, c.nn, nonnull, rg_rows, c.nn ? d_nonnull : nullptr, &c);
+        in_lane = false;
+        ctx = base;
+      }
+      // the waiting children, level by level (pre-order within a level: the
+      // columns of an earlier sibling come first, so after an inline failure
+      // the earlier siblings' children still run and report theirs first)
+      const int fork_rc = rc;
+      const uint32_t fork_col = err_col;
+      const std::string fork_msg = last_error;
+      while (!level.empty()) {
+        std::vector<Pending> cur;
+        cur.swap(level);
+        if (fork_rc) {
+          // only the children of columns before the failing one
+          size_t keep = 0;
+          while (keep < cur.size() && cur[keep].id < fork_col) ++keep;
+          cur.resize(keep);
+          if (cur.empty()) break;
+        }
+        std::vector<uint64_t> totals(cur.size(), 0);
+        int lr = read_back_lanes(cur, totals.data());
+        for (size_t q = 0; q < cur.size() && !lr; ++q) {
+          ctx = cur[q].lane;
+          in_lane = true;
+          if (fork_rc) err_col = kNoCol;  // an earlier column's inline failure comes first
+          for (uint32_t st : footer.types[cur[q].id].subtypes)
+            if ((lr = decode(st, totals[q], nullptr, totals[q], cur[q].child_rows))) break;
+          in_lane = false;
+          ctx = base;
+        }
+        if (lr) {
+          rc = lr;
+          break;
+        }
+      }
+      pending = nullptr;
+      if (fork_rc && rc == fork_rc && err_col == kNoCol) {
+        err_col = fork_col;
+        last_error = fork_msg;
+      }
+      for (unsigned l = 0; l < nl; ++l) {
+        if (!used[l]) continue;
+        int jr = hip_check(base, hipEventRecord(base->ev_join[l], base->lanes[l]->stream), "join event");
+        if (!jr) jr = hip_check(base, hipStreamWaitEvent(base->stream, base->ev_join[l], 0), "join wait");
+        if (jr && !rc) rc = fail_ctx(jr);
+      }
+      if (rc) return rc;
+    }
   } else if (k == ORCG_TYPE_UNION) {
     // UnionColumnReader (ColumnReader.cc:1158-1274): byte-RLE tags for the
     // non-null rows; each row's offset is its rank among the rows of its
@@ -1547,9 +1673,7 @@ struct HostSlab {
   std::vector<ColOut> out;  // host pointers into h
   int rc = ORCG_OK;
   std::string err;
-  ~HostSlab() {
-    if (h) (void)hipHostFree(h);
-  }
+  ~HostSlab() { pinned_free(h); }
 };
 
 // The buffers of a decoded column, in the batch layout of
@@ -1682,12 +1806,11 @@ struct orcg_row_reader {
     for (auto& bb : bufs) total += (bb.second.second + 255) & ~(uint64_t)255;
     if (total > sl.cap) {
       const double ta = now_s();
-      if (sl.h) (void)hipHostFree(sl.h);
+      pinned_free(sl.h);
       sl.h = nullptr;
       sl.cap = 0;
       const uint64_t ncap = std::max<uint64_t>(total + (total >> 3), 1 << 20);
-      if (hipHostMalloc((void**)&sl.h, ncap, hipHostMallocDefault) != hipSuccess)
-        return r->fail(ORCG_OUT_OF_MEMORY, "pinned row batch allocation failed");
+      if (!(sl.h = (uint8_t*)pinned_alloc(ncap))) return r->fail(ORCG_OUT_OF_MEMORY, "pinned row batch allocation failed");
       sl.cap = ncap;
       addp(3, now_s() - ta);
     }

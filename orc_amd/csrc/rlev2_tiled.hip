@@ -2337,9 +2337,26 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
         fprintf(stderr, "rle job: instance %d bytes %llu values %llu segments %llu (%.3f B/value)\n", v,
                 (unsigned long long)J.src_len, (unsigned long long)J.nvalues, (unsigned long long)J.nsegs,
                 (double)J.src_len / (double)J.nvalues);
+  // the instances' launches run concurrently on side streams (each is a few
+  // hundred to a couple of thousand workgroups of serial walks: together
+  // they fill the chip better than one after the other)
+  int ninst = 0;
+  for (int v = 2; v <= 7; ++v) ninst += group[v].empty() ? 0 : 1;
+  const bool par = ninst > 1 && side_lanes() > 1 && ctx_lane(ctx, (size_t)ninst - 1) != nullptr;
+  if (par) {
+    const int rc = hip_check(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork event");
+    if (rc) return rc;
+  }
+  Ctx* const base = ctx;
+  int li = 0;
   for (int v = 2; v <= 7; ++v) {
     std::vector<RleJob>& g = group[v];
     if (g.empty()) continue;
+    if (par) {
+      ctx = base->lanes[li++];
+      const int rc = hip_check(base, hipStreamWaitEvent(ctx->stream, base->ev_fork, 0), "fork wait");
+      if (rc) return rc;
+    }
     // workgroups start in index order: the streams with the most stream
     // bytes per value (the most runs per segment, the slowest segments) first,
     // so the launch does not end on a tail of slow segments
@@ -2357,6 +2374,21 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
     int rc = stage_jobs(ctx, g.data(), (uint32_t)g.size(), &d);
     if (!rc) rc = launch_tiled(ctx, v, nullptr, 0, 0, nullptr, segs, false, 0, 0, values, nullptr, 8, d,
                                (uint32_t)g.size());
+    if (rc) {
+      if (ctx != base) base->last_error = ctx->last_error;
+      ctx = base;
+      if (par)  // still join what was forked
+        for (int k = 0; k < li; ++k) {
+          (void)hipEventRecord(base->ev_join[k], base->lanes[k]->stream);
+          (void)hipStreamWaitEvent(base->stream, base->ev_join[k], 0);
+        }
+      return rc;
+    }
+  }
+  ctx = base;
+  for (int k = 0; par && k < li; ++k) {
+    int rc = hip_check(ctx, hipEventRecord(ctx->ev_join[k], ctx->lanes[k]->stream), "join event");
+    if (!rc) rc = hip_check(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join[k], 0), "join wait");
     if (rc) return rc;
   }
   return ORCG_OK;
