@@ -244,6 +244,12 @@ Ctx* ctx_lane(Ctx* base, size_t k) {
 using namespace orcg;
 
 
+namespace orcg {
+uint32_t host_parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_len, uint64_t* run_end) {
+  return parse_run(s, len, pos, run_len, run_end);
+}
+}  // namespace orcg
+
 orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes,
                                   uint64_t max_values) {
   auto* p = new orcg_rlev2_plan();

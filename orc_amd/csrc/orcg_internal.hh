@@ -212,6 +212,10 @@ struct orcg_rlev2_plan {
 };
 
 orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
+namespace orcg {
+// The RLEv2 run at `pos` (host): kErrNone with its value count and end, or a DevErr.
+uint32_t host_parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_len, uint64_t* run_end);
+}  // namespace orcg
 orcg_rlev2_plan* make_v1_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
 orcg_rlev2_plan* make_byte_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
 // H2D + RLEv2 decode of the first `count` values + D2H into host `out`.

@@ -1175,6 +1175,26 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
 // stripe): stripe footer (Reader.cc getStripeFooter :620-640), stream
 // location (StripeStream.cc:82-125), decompression of every selected stream
 // (Compression.cc) in parallel chunks, run plans + segment tables.
+// Whether an RLEv2 stream's first runs (up to 32) average >= 96 bytes: a
+// stream of long DIRECT / PATCHED_BASE runs (header bytes only are read).
+static bool fine_plans() {
+  static const bool on = [] {
+    const char* e = getenv("ORCG_FINE_PLANS");  // A/B: 0 keeps the row index for every RLEv2 stream
+    return !(e && atoi(e) == 0);
+  }();
+  return on;
+}
+static bool long_runs(const uint8_t* p, uint64_t len) {
+  uint64_t pos = 0, runs = 0;
+  while (pos < len && runs < 32) {
+    uint64_t L = 0, end = 0;
+    if (host_parse_run(p, len, pos, &L, &end) != kErrNone) return false;
+    pos = end;
+    ++runs;
+  }
+  return runs > 0 && pos >= 96 * runs;
+}
+
 int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   hs.stripe = s;
   hs.rc = ORCG_OK;
@@ -1425,14 +1445,34 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
       // on the host). Integer streams keep the row index: their host walk
       // chases run headers ~2 KB apart through memory (~45 ns a run, 0.9 ms
       // for a 42 MB stream), which lands on the host-bound critical path
+      //
+      // A nullable column's RLEv2 stream of long runs (its first runs
+      // average >= 96 bytes: DIRECT / PATCHED_BASE runs of hundreds of
+      // values) gets a host plan with 8 KB segments too: a child column's row
+      // group holds ~40,000 values in several serial window passes of one
+      // workgroup (C5's list items and map values: 260 workgroups per
+      // stream), while the host walk costs ~45 ns a run, a few thousand runs
+      // a stripe. Columns without nulls keep the row index: their streams
+      // share one multi-stream launch with the short-run streams, whose
+      // latency sets its length, and the extra host walk lands on the
+      // host-bound wall (C4: device 3.46 -> 3.64 ms, host plans 3.4 -> 7.8 ms
+      // with fine plans on every long-run stream).
+      bool fine = false;
       if (sb.pos) {
         const uint64_t per_group = hs.ngroups ? sb.len / hs.ngroups : 0;
-        if (kind != 0 || per_group <= (2u << 10)) continue;
+        if (kind == 0) {
+          if (per_group <= (2u << 10)) continue;
+        } else if (kind == 2 && fine_plans() && c.s[kSlotPresent].present && per_group > (8u << 10) &&
+                   long_runs(hs.h + sb.host_off, sb.len)) {
+          fine = true;
+        } else {
+          continue;
+        }
         sb.pos = false;
         sb.trip.clear();
       }
       rle.push_back(&sb);
-      rle_kind.push_back(kind);
+      rle_kind.push_back(fine ? 3 : kind);
     }
   }
   parallel_for(rle.size(), [&](size_t q) {
@@ -1441,6 +1481,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     // byte / boolean RLE without row-index segments: 1 KB segments (one wave each: enough waves to fill the GPU)
     if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, 1u << 10, 1024));
     else if (rle_kind[q] == 1) sb.plan.reset(make_v1_plan(p, sb.len, 16u << 10, 8192));
+    else if (rle_kind[q] == 3) sb.plan.reset(make_plan(p, sb.len, 8u << 10, 4096));
     else sb.plan.reset(make_plan(p, sb.len, 16u << 10, 8192));
   });
   hs.n_plan = rle.size();

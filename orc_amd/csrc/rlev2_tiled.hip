@@ -74,6 +74,15 @@ constexpr uint32_t kBlk = kSlab / kThreads;  // 8 bytes per thread
 constexpr uint32_t kDenseRuns = kSlab / 2;   // every run is >= 2 bytes
 constexpr uint32_t kStage = 256;             // values staged per wave
 constexpr uint32_t kShortL = 16;             // runs of <= kShortL values go lane-per-run
+constexpr uint32_t kVparL = 256;             // dense expansion: runs of kVparMin+1 .. kVparL values go
+#ifndef ORCG_VPAR_MIN                         // value-parallel
+#define ORCG_VPAR_MIN 16
+#endif
+constexpr uint32_t kVparMin = ORCG_VPAR_MIN;
+#ifndef ORCG_VPAR_FRAG
+#define ORCG_VPAR_FRAG 2
+#endif
+constexpr uint32_t kVparFrag = ORCG_VPAR_FRAG;  // short-run groups per 64 runs before all go value-parallel
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr uint32_t kDpErr = 0x80000000u;     // DP entry: a corrupt run starts here
 constexpr uint16_t kSink = 0xffffu;          // chain successor: none
@@ -1380,7 +1389,20 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     } else {
       run = parse_run([&](uint32_t i) { return lds_byte(win, hoff + i); }, ~0ull, kHdrLim, is_signed);
     }
-    const bool shortr = act && run.kind != 2 && run.L <= kShortL;
+    // SHORT_REPEAT, DIRECT and constant-step DELTA runs of kVparMin + 1 ..
+    // kVparL values are expanded value-parallel (below); short runs (<=
+    // kShortL) one lane per run through the stage; the rest (long runs,
+    // PATCHED_BASE) by the whole wave each
+    // Short runs stay one lane per run (their stage flush needs them
+    // consecutive) unless the longer runs between them cut them into more
+    // than kVparFrag groups (low-cardinality dictionary indices: a flush per
+    // group of a few runs); then every eligible run goes value-parallel
+    const bool elig = act && run.L <= kVparL && (run.kind <= 1 || (run.kind == 3 && run.W == 0));
+    const bool sh0 = act && run.kind != 2 && run.L <= kShortL;
+    const uint64_t shm = __ballot(sh0);
+    const bool frag = (uint32_t)__builtin_popcountll(shm & ~(shm << 1)) > kVparFrag;
+    const bool vpr = elig && (run.L > kVparMin || frag);
+    const bool shortr = sh0 && !vpr;
     const uint32_t Ls = shortr ? run.L : 0u;
     const uint32_t incl = wave_scan_u32(Ls);
     constexpr bool kStraight = (kOpt & kOptDirect) != 0;
@@ -1391,7 +1413,55 @@ __device__ __forceinline__ void dense_expand(const uint32_t* win, uint32_t nword
     // straight), then each long / PATCHED_BASE run by the whole wave, once
     // the parsed runs are dead (fewer live registers around expand_run)
     const uint32_t nact = r1 - c < (uint32_t)kWave ? r1 - c : (uint32_t)kWave;
-    const uint64_t longm = __ballot(act && !shortr);
+    const uint64_t longm = __ballot(act && !vpr && !shortr);
+    {
+      // value-parallel: lane o of each step takes value o of the runs'
+      // concatenation, finds its run by a binary search over the runs' first
+      // values (ds_bpermute, 6 steps), and decodes it by random access (a
+      // lane per run left most lanes idle behind the longest run of the 64,
+      // and runs of 17-256 values went one whole-wave expansion each: the
+      // low-cardinality dictionary indices of C4 spent 120 us a workgroup
+      // here)
+      const uint32_t Lv = vpr ? run.L : 0u;
+      const uint32_t inclv = wave_scan_u32(Lv);
+      const uint32_t exclv = inclv - Lv;
+      const uint32_t Tv = rdlane(inclv, kWave - 1);
+      if (Tv) {
+        const uint32_t pk = (hoff + run.data) | (run.W << 16) | (run.kind << 24);
+        const uint32_t a_lo = (uint32_t)run.a, a_hi = (uint32_t)(run.a >> 32);
+        const bool anyd = __ballot(vpr && run.kind == 3) != 0;
+        for (uint32_t o = (uint32_t)lane; __ballot(o < Tv) != 0; o += kWave) {
+          uint32_t lo = 0, hi = kWave;
+#pragma unroll
+          for (int st = 0; st < 6; ++st) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint32_t e = (uint32_t)__shfl((int)exclv, (int)mid);
+            if (e <= o) lo = mid;
+            else hi = mid;
+          }
+          const uint32_t k = lo;
+          const uint32_t p = (uint32_t)__shfl((int)pk, (int)k), e = (uint32_t)__shfl((int)exclv, (int)k);
+          const uint32_t vk = (uint32_t)__shfl((int)val, (int)k);
+          const uint64_t ak = (uint64_t)(uint32_t)__shfl((int)a_lo, (int)k) |
+                              (uint64_t)(uint32_t)__shfl((int)a_hi, (int)k) << 32;
+          const uint32_t j = o - e, kind = p >> 24;
+          uint64_t x = ak;
+          if (kind == 1) {
+            const uint32_t W = (p >> 16) & 0xffu, bit = j * W, br = (p & 0xffffu) + (bit >> 3);
+            const uint64_t v = field(lds12(win, br), br, bit & 7u, W);
+            x = is_signed ? unzigzag(v) : v;
+          }
+          if (anyd) {
+            const uint64_t bk = (uint64_t)(uint32_t)__shfl((int)(uint32_t)run.b, (int)k) |
+                                (uint64_t)(uint32_t)__shfl((int)(uint32_t)(run.b >> 32), (int)k) << 32;
+            if (kind == 3) x = ak + (uint64_t)j * bk;
+          }
+          const uint64_t g = vi + vk + j;
+          if (o < Tv && g >= value_begin && g < value_end) store1<kOpt>(dst + (g - value_begin), x);
+        }
+        ORCG_COVER_ADD(vpr ? run.L : 0u);
+      }
+    }
     for (uint64_t rem = __ballot(shortr); rem;) {
       const uint32_t a = (uint32_t)__builtin_ctzll(rem);
       // short runs [a, b): consecutive in the output; a stage-full at most
@@ -2135,6 +2205,21 @@ static int default_variant(uint64_t src_len, uint64_t est_values) {
 // One launch (or serial + drain pair) of instance `variant` over nsegs
 // segments of one stream, or (jobs_d) over the launch-wide segments of a
 // device job table.
+// ORCG_DEBUG_DEFER: after a serial launch, how many of its segments it
+// queued for the dense drain (stderr; synchronises the stream)
+static void debug_defer(Ctx* ctx, const unsigned long long* dq, uint64_t nsegs, uint32_t dpar) {
+  static const bool on = getenv("ORCG_DEBUG_DEFER") != nullptr;
+  if (!on) return;
+  std::vector<unsigned long long> h(3 * nsegs + 1);
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
+      hipMemcpy(h.data(), dq, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  uint64_t q = 0;
+  for (uint64_t g = 0; g < nsegs; ++g) q += h[3 * g] == dpar ? 1 : 0;
+  fprintf(stderr, "defer: %llu of %llu segments queued (any %d)\n", (unsigned long long)q,
+          (unsigned long long)nsegs, h[3 * nsegs] == dpar ? 1 : 0);
+}
+
 static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode, uint64_t rows_per_group,
                         uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes, const RleJob* jobs_d,
@@ -2213,6 +2298,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     if (rc_) return rc_;                                                            \
     dpar = (uint32_t)(ctx->defer_seq++ % 0xffffffffull) + 1u; /* never 0 */         \
     ORCG_KX(O, WKB, false, MWV, 0, 1, (unsigned)nsegs);                              \
+    debug_defer(ctx, dq, nsegs, dpar);                                                \
     ORCG_KX(DO, 8, false, 6, 2, 2, drain);                                           \
   } while (0)
 

@@ -161,6 +161,7 @@ def main():
                          "host): device decode at steady clocks; 0 = skip")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; gloo lets "
                                                       "ranks share one GPU)")
+    ap.add_argument("--variant", type=int, default=0, help="pinned RLEv2 kernel variant (0 = per-stream default)")
     ap.add_argument("--check", default="all", choices=["all", "first", "none"],
                     help="stripes of this rank checked against pyarrow outside the timed region (numpy on the "
                          "value buffers, tests/arrow_parity.py)")
@@ -198,6 +199,8 @@ def main():
     from orc_amd.shard import reader_ranges
 
     ctx = orc_amd.Context(local_rank % max(torch.cuda.device_count(), 1))
+    if args.variant:
+        ctx.set_rlev2_variant(args.variant)
     r = orc_amd.Reader(path, ctx)
     if args.no_batch:
         r.set_stream_batching(False)
