@@ -141,6 +141,69 @@ def row_reader_leg(path, nrows, stripes_wall):
     return out
 
 
+def multi_reader_leg(path, k, first, last, stripe_rows, iters, device):
+    """k Readers, each with its own Context (stream), read contiguous stripe
+    ranges of [first, last) from k threads (ctypes drops the GIL in the
+    library calls); the decoded batches stay in HBM as in the single-reader
+    pass (checked by check_multi, outside the timed region)."""
+    import threading
+
+    import orc_amd
+
+    bounds = np.linspace(first, last, k + 1).round().astype(int)
+    parts = [(int(a), int(b)) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
+    readers = [orc_amd.Reader(path, orc_amd.Context(device)) for _ in parts]
+    errs = []
+
+    def one(rd, a, b):
+        try:
+            rd.read_stripes_device(a, b - a)
+        except Exception as e:  # surfaced after the join
+            errs.append(e)
+
+    def scan():
+        ts = [threading.Thread(target=one, args=(rd, a, b)) for rd, (a, b) in zip(readers, parts)]
+        t = time.perf_counter()
+        for th in ts:
+            th.start()
+        for th in ts:
+            th.join()
+        dt = time.perf_counter() - t
+        if errs:
+            raise errs[0]
+        return dt
+
+    scan()  # warm-up (allocations)
+    wall = min(scan() for _ in range(max(iters, 1)))
+    rows = int(sum(stripe_rows[first:last]))
+    return {"readers": len(parts), "wall_s": round(wall, 4), "mrows_per_s": round(rows / wall / 1e6, 2),
+            "ranges": parts if len(parts) <= 16 else len(parts)}, readers, parts
+
+
+def check_multi(readers, parts, r, first):
+    """The concurrent scan's resident batches (every stripe, every column)
+    against the single reader's batches of the same stripes."""
+    for rd, (a, b) in zip(readers, parts):
+        for s in range(a, b):
+            for t in r.types:
+                v1, v0 = rd.stripe_column_view(s - a, t.id), r.stripe_column_view(s - first, t.id)
+                if v1.decoded != v0.decoded:
+                    return "stripe %d column %d: decoded flag differs" % (s, t.id)
+                if v0.decoded and not _same(vars(rd._column(v1, t)), vars(r._column(v0, t))):
+                    return "stripe %d column %d differs" % (s, t.id)
+    return None
+
+
+def _same(a, b):
+    if isinstance(a, np.ndarray) or isinstance(b, np.ndarray):
+        return np.array_equal(np.asarray(a), np.asarray(b))
+    if isinstance(a, (list, tuple)) and isinstance(b, (list, tuple)):
+        return len(a) == len(b) and all(_same(x, y) for x, y in zip(a, b))
+    if isinstance(a, dict) and isinstance(b, dict):
+        return a.keys() == b.keys() and all(_same(a[x], b[x]) for x in a)
+    return a == b
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
@@ -162,6 +225,10 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL; gloo lets "
                                                       "ranks share one GPU)")
     ap.add_argument("--variant", type=int, default=0, help="pinned RLEv2 kernel variant (0 = per-stream default)")
+    ap.add_argument("--readers", type=int, default=0,
+                    help="also time a scan by this many Readers (each its own Context and stream) on contiguous "
+                         "stripe ranges (RowReaderOptions::range), driven from as many host threads: small "
+                         "stripes' fixed costs overlap on one GPU")
     ap.add_argument("--check", default="all", choices=["all", "first", "none"],
                     help="stripes of this rank checked against pyarrow outside the timed region (numpy on the "
                          "value buffers, tests/arrow_parity.py)")
@@ -256,6 +323,16 @@ def main():
             if v.decoded:
                 dec_bytes += view_bytes(v, t.kind, t.precision)
 
+    multi = None
+    if args.readers > 1 and rank == 0:
+        multi, mreaders, mparts = multi_reader_leg(path, args.readers, first, last, stripe_rows, args.iters,
+                                                   ctx.device)
+        diff = check_multi(mreaders, mparts, r, first)
+        if diff:
+            raise SystemExit("multi-reader scan differs from the single reader: " + diff)
+        multi["check"] = "every stripe and column equal to the single reader's resident batches"
+        del mreaders
+
     concat = None
     if dist:
         concat = concat_leg(dist, r, path, first, last, rank)
@@ -343,6 +420,7 @@ def main():
                                   1)),
             "host_batch_copy_s": None if host is None else round(host, 3),
             "concat": concat,
+            "multi_reader": multi,
             "row_reader": rowreader,
             "check": check,
             "cpu_baseline": cpu,

@@ -128,6 +128,51 @@ def test_pipelined_multi_stripe_read_matches_pyarrow(ctx, name):
         np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("name", ["demo-11-zlib.orc", "nulls-at-end-snappy.orc"])
+def test_concurrent_readers_on_stripe_ranges(ctx, name):
+    """Four Readers, each with its own Context, read contiguous stripe ranges
+    (RowReaderOptions::range, Reader.cc:337-345) from four threads at once
+    (bench_file.py --readers): every resident batch equals the single
+    reader's pipelined read of the same stripes."""
+    import threading
+
+    r = orc_amd.Reader(path(name), ctx)
+    r.read_stripes_device()
+    n = r.num_stripes
+    bounds = np.linspace(0, n, 5).round().astype(int)
+    parts = [(int(a), int(b)) for a, b in zip(bounds[:-1], bounds[1:]) if b > a]
+    readers = [orc_amd.Reader(path(name), orc_amd.Context(0)) for _ in parts]
+    errs = []
+
+    def one(rd, a, b):
+        try:
+            for _ in range(3):  # repeated scans: each one overlaps the others' launches
+                rd.read_stripes_device(a, b - a)
+        except Exception as e:
+            errs.append(e)
+
+    ts = [threading.Thread(target=one, args=(rd, a, b)) for rd, (a, b) in zip(readers, parts)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    for rd, (a, b) in zip(readers, parts):
+        for s in range(a, b):
+            for t in r.types:
+                v1, v0 = rd.stripe_column_view(s - a, t.id), r.stripe_column_view(s, t.id)
+                assert v1.decoded == v0.decoded
+                if not v0.decoded:
+                    continue
+                c1, c0 = vars(rd._column(v1, t)), vars(r._column(v0, t))
+                for key in c0:
+                    x, y = c1[key], c0[key]
+                    if isinstance(y, np.ndarray) or isinstance(x, np.ndarray):
+                        np.testing.assert_array_equal(x, y, err_msg="stripe %d column %d %s" % (s, t.id, key))
+                    else:
+                        assert x == y, (s, t.id, key)
+
+
 @pytest.mark.parametrize("name", ["demo-12-zlib.orc", "TestOrcFile.test1.orc", "nulls-at-end-snappy.orc",
                                   "complextypes_iceberg.orc", "TestVectorOrcFile.testLz4.orc",
                                   "orc-file-11-format.orc", "decimal.orc"])
