@@ -46,15 +46,16 @@ def test_file_matches_pyarrow(ctx, name):
     assert diff is None, "%s: %s" % (name, diff)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 6, 16, 20])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("name", ["nulls-at-end-snappy.orc", "TestOrcFile.test1.orc", "orc_index_int_string.orc",
                                   "TestStringDictionary.testRowIndex.orc"])
 def test_row_indexed_file_under_pinned_variant(name, variant):
     """Row-indexed files (row-group segment tables for their RLEv2 streams)
-    under every pinned kernel variant, including the wave walk (1) and the
-    instances that take no multi-stream job table (16, 20): the same rows as
-    pyarrow (VERDICT r03 #4, ADVICE r02)."""
+    under every variant the shipped library pins (orc_amd.rlev2_variants()),
+    including the wave walk (1): the same rows as pyarrow (VERDICT r03 #4,
+    ADVICE r02)."""
     pytest.importorskip("pyarrow.orc")
+    assert variant in orc_amd.rlev2_variants()
     c = orc_amd.Context(0)
     c.set_rlev2_variant(variant)
     r, fields, got = _read_all(c, name)
