@@ -245,7 +245,16 @@ def main():
     t0 = time.time()
     if rank == 0 and maker is not None and not os.path.exists(path):
         progress("writing %s (%d rows)" % (path, rows))
-        maker(path + ".tmp", rows, args.stripe_mb)
+        import threading
+
+        w = threading.Thread(target=maker, args=(path + ".tmp", rows, args.stripe_mb))
+        w.start()
+        while w.is_alive():  # a line every 30 s: a 10^8-row file takes minutes to write
+            w.join(30)
+            if w.is_alive():
+                progress("still writing %s" % path)
+        if not os.path.exists(path + ".tmp"):
+            raise SystemExit("writing %s failed" % path)
         os.replace(path + ".tmp", path)
     t_make = time.time() - t0
 

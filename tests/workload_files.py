@@ -75,8 +75,14 @@ def make_c4(path, rows, stripe_mb, row_index_stride=10000, compression="zstd"):
     ship = rng.integers(8036, 10561, size=rows).astype(np.int32)  # 1992-01-02 .. 1998-12-01
     pool = pa.array(["".join(chr(97 + c) for c in rng.integers(0, 26, size=int(rng.integers(5, 22))))
                      for _ in range(4096)])
-    c1 = pc.take(pool, pa.array(rng.integers(0, 4096, size=rows)))
-    c2 = pc.take(pool, pa.array(rng.integers(0, 4096, size=rows)))
+    i1 = rng.integers(0, 4096, size=rows)
+    i2 = rng.integers(0, 4096, size=rows)
+    # l_comment in chunks of 8M rows: an Arrow string array holds < 2 GiB
+    # (configs[3]'s 1.25 * 10^8 rows per GPU make ~3.4 GB of comments)
+    step = 1 << 23
+    comment = pa.chunked_array([pc.binary_join_element_wise(pc.take(pool, pa.array(i1[a:a + step])),
+                                                            pc.take(pool, pa.array(i2[a:a + step])), " ")
+                                for a in range(0, rows, step)], type=pa.string())
     table = pa.table({
         "l_orderkey": pa.array(okey),
         "l_partkey": pa.array(rng.integers(1, 20_000_001, size=rows)),
@@ -94,7 +100,7 @@ def make_c4(path, rows, stripe_mb, row_index_stride=10000, compression="zstd"):
         "l_shipinstruct": _dict_strings(pa, rng, ["DELIVER IN PERSON", "COLLECT COD", "NONE",
                                                   "TAKE BACK RETURN"], rows),
         "l_shipmode": _dict_strings(pa, rng, ["REG AIR", "AIR", "RAIL", "SHIP", "TRUCK", "MAIL", "FOB"], rows),
-        "l_comment": pc.binary_join_element_wise(c1, c2, " "),
+        "l_comment": comment,
     })
     po.write_table(table, path, compression=compression, stripe_size=stripe_mb << 20,
                    dictionary_key_size_threshold=0.5, row_index_stride=row_index_stride)
