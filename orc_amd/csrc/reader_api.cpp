@@ -1182,6 +1182,17 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
 // (Compression.cc) in parallel chunks, run plans + segment tables.
 // Whether an RLEv2 stream's first runs (up to 32) average >= 96 bytes: a
 // stream of long DIRECT / PATCHED_BASE runs (header bytes only are read).
+// Streams up to this many bytes take a host plan even with a row index
+// (ORCG_SMALL_STREAM, bytes; 0 = never): walking a few KB of run headers
+// costs the host microseconds, and the plan's segment table rides in the
+// stripe's upload, where the row-index path launches rg_segtab (and
+// rg_prefix under a mask) per stream. configs[0]'s 5,000-row stripes: ~30
+// launches per stripe, a third of them segment tables.
+static uint64_t small_stream_bytes() {
+  const char* e = getenv("ORCG_SMALL_STREAM");
+  return e ? strtoull(e, nullptr, 10) : (64u << 10);
+}
+
 static bool fine_plans() {
   static const bool on = [] {
     const char* e = getenv("ORCG_FINE_PLANS");  // A/B: 0 keeps the row index for every RLEv2 stream
@@ -1428,6 +1439,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   // host run plans (header walks only) for every RLE stream, in parallel
   std::vector<StreamBuf*> rle;
   std::vector<int> rle_kind;  // 0 byte RLE, 1 RLEv1, 2 RLEv2
+  const uint64_t small = small_stream_bytes();
   for (size_t i = 0; i < nt; ++i) {
     Col& c = hs.cols[i];
     if (!selected[i] || !c.supported) continue;
@@ -1472,7 +1484,9 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
       bool fine = false;
       if (sb.pos) {
         const uint64_t per_group = hs.ngroups ? sb.len / hs.ngroups : 0;
-        if (kind == 0) {
+        if (sb.len <= small) {
+          // small stream: a host plan (small_stream_bytes)
+        } else if (kind == 0) {
           if (per_group <= (2u << 10)) continue;
         } else if (kind == 2 && fine_plans() && c.s[kSlotPresent].present && per_group > (8u << 10) &&
                    long_runs(hs.h + sb.host_off, sb.len)) {
