@@ -1182,15 +1182,15 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
 // (Compression.cc) in parallel chunks, run plans + segment tables.
 // Whether an RLEv2 stream's first runs (up to 32) average >= 96 bytes: a
 // stream of long DIRECT / PATCHED_BASE runs (header bytes only are read).
-// Streams up to this many bytes take a host plan even with a row index
-// (ORCG_SMALL_STREAM, bytes; 0 = never): walking a few KB of run headers
-// costs the host microseconds, and the plan's segment table rides in the
-// stripe's upload, where the row-index path launches rg_segtab (and
-// rg_prefix under a mask) per stream. configs[0]'s 5,000-row stripes: ~30
-// launches per stripe, a third of them segment tables.
+// A/B (ORCG_SMALL_STREAM=bytes; default 0 = never): streams up to this many
+// bytes take a host plan even with a row index, so their segment table rides
+// in the stripe's upload instead of an rg_segtab launch (+ rg_prefix under a
+// mask) per stream. Measured at 64 KB on configs[0] (9 of its 38 launches
+// per 5,000-row stripe): device decode 0.2337 vs 0.2332 s over the file, the
+// segment-table launches overlap the chain; not the bound, so off.
 static uint64_t small_stream_bytes() {
   const char* e = getenv("ORCG_SMALL_STREAM");
-  return e ? strtoull(e, nullptr, 10) : (64u << 10);
+  return e ? strtoull(e, nullptr, 10) : 0;
 }
 
 static bool fine_plans() {

@@ -197,8 +197,8 @@ def test_row_index_segments_match_host_plans(ctx, name, monkeypatch):
     """Streams cut at row groups by the ROW_INDEX positions (no host header
     walk) decode exactly like the host-planned segmentation, and both equal
     pyarrow's ORC C++ reader (the reference) on every decodable field.
-    ORCG_SMALL_STREAM=0 keeps the row index for these small files' streams
-    (by default streams up to 64 KB take host plans)."""
+    ORCG_SMALL_STREAM=0 (the default) keeps the row index for these small
+    files' streams."""
     monkeypatch.setenv("ORCG_SMALL_STREAM", "0")
     r = orc_amd.Reader(path(name), ctx)
     got = [r.read_stripe(s) for s in range(r.num_stripes)]
