@@ -224,6 +224,34 @@ int orcg_reader_last_timings(const orcg_reader* r, double* out5);
  * (ColumnReader::seekToRowGroup's PositionProvider, no host work) [0] and by
  * a host header walk (files without a row index) [1]. */
 int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2);
+/* ReaderMetrics (c++/include/orc/Reader.hh:59-76; ReaderOptions::setReaderMetrics),
+ * accumulated over the reader's life by every decode (read_stripe,
+ * read_stripes, row readers). One "reader call" / "I/O" is one stripe read
+ * (its byte range of the file); decompression counts compression chunks and
+ * their host time; decoding counts RLE streams (RLEv1 / RLEv2 launches and
+ * multi-stream jobs) with the device decode phase as its latency; byte decoding
+ * counts byte / boolean RLE streams, whose kernels run inside that phase (their
+ * latency is not split out: 0). Row groups: selected = the decoded stripes'
+ * row groups (no search arguments, so evaluated stays 0), as do the read-range
+ * cache counters. */
+typedef struct orcg_reader_metrics {
+  uint64_t reader_call;
+  uint64_t reader_inclusive_latency_us;
+  uint64_t decompression_call;
+  uint64_t decompression_latency_us;
+  uint64_t decoding_call;
+  uint64_t decoding_latency_us;
+  uint64_t byte_decoding_call;
+  uint64_t byte_decoding_latency_us;
+  uint64_t io_count;
+  uint64_t io_blocking_latency_us;
+  uint64_t selected_row_group_count;
+  uint64_t evaluated_row_group_count;
+  uint64_t read_range_cache_hits;
+  uint64_t read_range_cache_misses;
+} orcg_reader_metrics;
+int orcg_reader_get_metrics(orcg_reader* r, orcg_reader_metrics* out);
+int orcg_reader_reset_metrics(orcg_reader* r);
 /* RLEv2 streams of the last read decoded by a stripe's multi-stream launches
  * (every stream whose value count is known on the host: one launch per
  * kernel instance per stripe instead of one per stream). */

@@ -165,6 +165,8 @@ SIGNATURES += [
     ("orcg_reader_copy_to_host", [vp, vp, vp, u64], i32),
     ("orcg_reader_last_timings", [vp, ctypes.POINTER(ctypes.c_double)], i32),
     ("orcg_reader_last_stream_stats", [vp, ctypes.POINTER(u64)], i32),
+    ("orcg_reader_get_metrics", [vp, ctypes.POINTER(u64)], i32),
+    ("orcg_reader_reset_metrics", [vp], i32),
     ("orcg_reader_content_length", [vp], u64),
     ("orcg_reader_software_version", [vp], cp),
     ("orcg_reader_num_metadata", [vp], u32),

@@ -213,6 +213,7 @@ struct HostStage {
   double t_parse = 0, t_decomp = 0, t_plan = 0;
   uint64_t ngroups = 0;    // row groups with row-index positions (0: host plans only)
   uint64_t n_pos = 0, n_plan = 0;  // RLE streams cut by the row index / by a host plan
+  uint64_t n_chunks = 0;            // compression chunks inflated (ReaderMetrics::DecompressionCall)
   uint64_t rows_off = 0;   // staging offset of int64 rows[g] = g * stride
   ~HostStage() { pinned_free(h); }
   bool ensure(uint64_t bytes, uint64_t keep) {
@@ -308,6 +309,9 @@ struct orcg_reader {
   DevSlot* D = nullptr;
   double timings[5] = {0, 0, 0, 0, 0};
   uint64_t stream_stats[2] = {0, 0};  // last read: RLE streams cut by the row index, by host plans
+  // ReaderMetrics (Reader.hh:59-76) over the reader's life, in orcg_reader_metrics
+  // order; updated under mu (every decode holds it)
+  uint64_t metrics[14] = {};
   uint64_t batched_streams = 0;       // last read: RLEv2 streams decoded by multi-stream launches
   uint64_t stage_bytes = 0;           // last read: bytes uploaded (decompressed streams + plans)
 
@@ -600,6 +604,7 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   int rc = segments(c, slot, false, &d_seg, &nseg);
   if (rc) return rc;
   const int sg = is_signed ? 1 : 0;
+  ++metrics[4];  // DecodingCall
   if (v1)
     rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
   else
@@ -640,6 +645,7 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
   j.is_signed = is_signed ? 1u : 0u;
   j.err = D->d_errs + id;
   batch.push_back(j);
+  ++metrics[4];  // DecodingCall
   batched[(uint64_t)id * 8 + (uint64_t)slot] = {out, count};
   return ORCG_OK;
 }
@@ -696,6 +702,7 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   uint64_t nseg;
   int rc = segments(c, slot, boolean, &d_seg, &nseg);
   if (rc) return rc;
+  ++metrics[6];  // ByteDecodingCall
   rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count);
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
@@ -1513,6 +1520,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     else sb.plan.reset(make_plan(p, sb.len, 16u << 10, 8192));
   }, plan_bytes, 512u << 10);  // header walks: ~512 KB of stream per thread
   hs.n_plan = rle.size();
+  hs.n_chunks = all.size();
   hs.n_pos = 0;
   for (auto& c : hs.cols)
     for (auto& sb : c.s) hs.n_pos += sb.pos ? 1 : 0;
@@ -1676,8 +1684,21 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   }
   H = nullptr;
   D = nullptr;
+  const double t_end = now_s();
   timings[3] += t1 - t0;
-  timings[4] += now_s() - t1;
+  timings[4] += t_end - t1;
+  // ReaderMetrics: one stripe read = one reader call and one I/O (the stripe's
+  // byte range of the mapped file); the host phases come from prepare()
+  const uint64_t stride = footer.row_index_stride;
+  const uint64_t srows = footer.stripes[hs.stripe].num_rows;
+  metrics[0] += 1;
+  metrics[1] += (uint64_t)((hs.t_parse + hs.t_decomp + hs.t_plan + (t_end - t0)) * 1e6);
+  metrics[2] += hs.n_chunks;
+  metrics[3] += (uint64_t)(hs.t_decomp * 1e6);
+  metrics[5] += (uint64_t)((t_end - t1) * 1e6);
+  metrics[8] += 1;
+  metrics[9] += (uint64_t)(hs.t_parse * 1e6);
+  metrics[10] += stride ? (srows + stride - 1) / stride : (srows ? 1 : 0);
   return rc;
 }
 
@@ -2454,6 +2475,21 @@ int orcg_reader_last_stream_stats(const orcg_reader* r, uint64_t* out2) {
 }
 
 uint64_t orcg_reader_last_batched_streams(const orcg_reader* r) { return r ? r->batched_streams : 0; }
+
+int orcg_reader_get_metrics(orcg_reader* r, orcg_reader_metrics* out) {
+  if (!r || !out) return ORCG_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(r->mu);
+  static_assert(sizeof(orcg_reader_metrics) == sizeof(r->metrics), "orcg_reader_metrics layout");
+  memcpy(out, r->metrics, sizeof(r->metrics));
+  return ORCG_OK;
+}
+
+int orcg_reader_reset_metrics(orcg_reader* r) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(r->mu);
+  memset(r->metrics, 0, sizeof(r->metrics));
+  return ORCG_OK;
+}
 uint64_t orcg_reader_last_stage_bytes(const orcg_reader* r) { return r ? r->stage_bytes : 0; }
 
 int orcg_reader_set_stream_batching(orcg_reader* r, int on) {

@@ -436,6 +436,21 @@ class Reader:
                 "batched": int(self._L.orcg_reader_last_batched_streams(self._h)),
                 "stage_bytes": int(self._L.orcg_reader_last_stage_bytes(self._h))}
 
+    METRIC_NAMES = ("ReaderCall", "ReaderInclusiveLatencyUs", "DecompressionCall", "DecompressionLatencyUs",
+                    "DecodingCall", "DecodingLatencyUs", "ByteDecodingCall", "ByteDecodingLatencyUs", "IOCount",
+                    "IOBlockingLatencyUs", "SelectedRowGroupCount", "EvaluatedRowGroupCount",
+                    "ReadRangeCacheHits", "ReadRangeCacheMisses")
+
+    def metrics(self, reset=False):
+        """ReaderMetrics (c++/include/orc/Reader.hh:59-76) accumulated over the
+        reader's life, keyed by the reference's member names
+        (orcg_reader_get_metrics); reset=True zeroes them afterwards."""
+        t = (ctypes.c_uint64 * len(self.METRIC_NAMES))()
+        check(self._L.orcg_reader_get_metrics(self._h, t))
+        if reset:
+            check(self._L.orcg_reader_reset_metrics(self._h))
+        return dict(zip(self.METRIC_NAMES, (int(x) for x in t)))
+
     def set_stream_batching(self, on=True):
         """Decode a stripe's host-countable RLEv2 streams with one launch per
         kernel instance (default) or one launch per stream."""

@@ -104,6 +104,25 @@ def test_device_views_and_timings(ctx):
     assert set(t) == {"host_parse_s", "host_decompress_s", "host_plan_s", "h2d_s", "device_decode_s"}
 
 
+def test_reader_metrics(ctx):
+    """ReaderMetrics (Reader.hh:59-76) through orcg_reader_get_metrics: one
+    reader call and one I/O per stripe read, chunks inflated, RLE and byte-RLE
+    streams decoded, the stripes' row groups; cumulative until reset."""
+    r = orc_amd.Reader(path("demo-11-zlib.orc"), ctx)
+    assert set(r.metrics().values()) == {0}
+    r.read_stripes_device(0, 3)
+    m = r.metrics()
+    assert m["ReaderCall"] == 3 and m["IOCount"] == 3
+    assert m["DecompressionCall"] > 0 and m["DecodingCall"] > 0
+    assert m["SelectedRowGroupCount"] == 3  # 5,000-row stripes, stride 10,000
+    assert m["ReaderInclusiveLatencyUs"] >= m["DecodingLatencyUs"]
+    assert m["EvaluatedRowGroupCount"] == 0
+    r.read_stripe(3)
+    m2 = r.metrics(reset=True)
+    assert m2["ReaderCall"] == 4 and m2["DecodingCall"] > m["DecodingCall"]
+    assert set(r.metrics().values()) == {0}
+
+
 def test_in_memory_source_matches_file(ctx):
     data = open(path("TestOrcFile.testSnappy.orc"), "rb").read()
     r1 = orc_amd.Reader(data, ctx)
