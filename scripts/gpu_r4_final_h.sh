@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-4 pass H (final tree): reader / workload GPU tests, smoke, the bench
+# round-4 pass H (final tree, with ReaderMetrics): reader / workload GPU tests, smoke, the bench
 # line, rocprof of bench.py, C1 single + 16 concurrent readers
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -15,7 +15,7 @@ run() {
   return $rc
 }
 export TMPDIR=/tmp
-run h_tests 400 python -u -m pytest tests/test_gpu_reader.py tests/test_gpu_workloads.py tests/test_gpu_row_reader.py tests/test_gpu_rlev2.py -m gpu -x -q --timeout 120 --timeout-method thread || exit 1
+run h_tests 500 python -u -m pytest tests/test_gpu_reader.py tests/test_gpu_workloads.py tests/test_gpu_row_reader.py tests/test_cxx_adapter.py tests/test_gpu_rlev2.py -m gpu -x -q --timeout 120 --timeout-method thread || exit 1
 run h_smoke 120 python __graft_entry__.py smoke || exit 1
 run h_bench 300 python bench.py || exit 1
 run h_prof 200 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/h_prof" -o run --output-format csv -- python3 bench.py --steps 50 --warmup 100 --no-cpu-baseline --no-verify --copy-inclusive 0 || exit 1
