@@ -186,6 +186,110 @@ __global__ __launch_bounds__(1024) void lengths_scan_kernel(const int64_t* __res
   }
 }
 
+// A stripe's dictionary string columns in one launch: per column the entry
+// offsets (loadStringDictionary's prefix sum and negative-length check,
+// DictionaryLoader.cc:69-80) and the row gather (StringDictionaryColumnReader::
+// next, ColumnReader.cc:561-594). Every workgroup scans its column's entry
+// lengths into LDS (dictionaries of <= kDictLds entries: a few KB) and
+// gathers one tile of rows from there; the column's first tile also writes
+// the offsets and the {blob bytes, negative length} summary. Null rows get
+// (0, 0), as the per-column path's memset leaves them.
+constexpr uint32_t kDictTile = 2048;  // rows per workgroup (256 threads x 8)
+
+// One workgroup per (column, tile): jobs[blockIdx.x] is the column's job with
+// tile_base = the tile's index in the column (the host writes one copy per
+// tile: a workgroup reads its whole description in one load). The tile's
+// indices are loaded before the dictionary's lengths so both latencies
+// overlap.
+__global__ __launch_bounds__(kThreads) void dict_multi_kernel(const DictJob* __restrict__ jobs, uint32_t njobs) {
+  __shared__ int64_t s_off[kDictLds + 1];
+  __shared__ uint64_t s_wsum[kThreads / kWave];
+  __shared__ uint32_t s_neg;
+  constexpr int kRows = kDictTile / kThreads;
+  const int tid = (int)threadIdx.x, lane = tid % kWave, wv = tid / kWave;
+  const DictJob& J = jobs[blockIdx.x];
+  const uint64_t tile = uni64(J.tile_base);
+  const uint64_t D = uni64(J.dict_size);
+  const uint64_t n = uni64(J.n);
+  const int64_t* lengths = (const int64_t*)uni64((uint64_t)(uintptr_t)J.lengths);
+  const int64_t* idx = (const int64_t*)uni64((uint64_t)(uintptr_t)J.idx);
+  const uint8_t* nn = (const uint8_t*)uni64((uint64_t)(uintptr_t)J.nn);
+  const uint64_t r0 = tile * kDictTile;
+  // my rows' entries (and not-null bytes) first
+  int64_t e_[kRows];
+  uint32_t present = 0;
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const uint64_t i = r0 + (uint64_t)k * kThreads + (uint64_t)tid;
+    const bool in = i < n;
+    const bool p = in && (!nn || nn[i] != 0);
+    present |= (p ? 1u : 0u) << k;
+    e_[k] = p ? idx[i] : 0;
+  }
+  if (tid == 0) s_neg = 0;
+  // offsets: thread t sums entries [16t, 16t + 16)
+  int64_t loc[16];
+  uint64_t sum = 0;
+  bool neg = false;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t e = 16u * (uint64_t)tid + k;
+    const int64_t x = e < D ? lengths[e] : 0;
+    neg |= x < 0;
+    loc[k] = (int64_t)sum;
+    sum += (uint64_t)x;
+  }
+  const uint64_t inc = wave_inclusive_scan(sum, lane);
+  if (lane == kWave - 1) s_wsum[wv] = inc;
+  if (__any(neg) && lane == 0) atomicOr(&s_neg, 1u);
+  __syncthreads();
+  uint64_t before = inc - sum, total = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / kWave; ++w) {
+    before += w < wv ? s_wsum[w] : 0ull;
+    total += s_wsum[w];
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t e = 16u * (uint64_t)tid + k;
+    if (e < D) s_off[e] = (int64_t)(before + (uint64_t)loc[k]);
+  }
+  if (tid == 0) s_off[D] = (int64_t)total;
+  __syncthreads();
+  if (tile == 0) {
+    int64_t* off = (int64_t*)uni64((uint64_t)(uintptr_t)J.offsets);
+    for (uint64_t e = (uint64_t)tid; e <= D; e += kThreads) off[e] = s_off[e];
+    if (tid == 0) {
+      uint64_t* sm = (uint64_t*)uni64((uint64_t)(uintptr_t)J.summary);
+      sm[0] = total;
+      sm[1] = s_neg;
+    }
+  }
+  if (r0 >= n) return;
+  int64_t* out_start = (int64_t*)uni64((uint64_t)(uintptr_t)J.start);
+  int64_t* out_len = (int64_t*)uni64((uint64_t)(uintptr_t)J.len);
+  unsigned long long* err = (unsigned long long*)uni64((uint64_t)(uintptr_t)J.err);
+#pragma unroll
+  for (int k = 0; k < kRows; ++k) {
+    const uint64_t i = r0 + (uint64_t)k * kThreads + (uint64_t)tid;
+    if (i >= n) break;
+    if (!((present >> k) & 1u)) {  // a null row
+      out_start[i] = 0;
+      out_len[i] = 0;
+      continue;
+    }
+    const uint64_t e = (uint64_t)e_[k];
+    if (e >= D) {
+      report(err, i, kErrDictIndex);
+      continue;
+    }
+    const int64_t st = s_off[e];
+    out_start[i] = st;
+    out_len[i] = s_off[e + 1] - st;
+  }
+  (void)njobs;
+}
+
 // Multi-workgroup exclusive scan of int64 values (lengths -> offsets):
 // per-tile sums, one-workgroup scan of the sums, per-tile scan. Used for
 // direct string lengths (DATA offsets, StringDirectColumnReader::next,
@@ -444,6 +548,38 @@ int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t
   else
     return set_error(ctx, ORCG_INVALID_ARGUMENT, "index width must be 8 or 4");
   return hip_check(ctx, hipGetLastError(), "dictionary gather launch");
+}
+
+int plan_dict_multi(Ctx* ctx, const DictJob* jobs, uint32_t njobs, std::vector<MultiLaunch>& out) {
+  // one copy of the column's job per tile of kDictTile rows (tile_base = the
+  // tile's index): a workgroup needs no search through the table
+  std::vector<DictJob> g;
+  for (uint32_t j = 0; j < njobs; ++j) {
+    if (jobs[j].dict_size > kDictLds) return set_error(ctx, ORCG_INVALID_ARGUMENT, "dictionary too large for a batch");
+    const uint64_t tiles = std::max<uint64_t>(1, (jobs[j].n + kDictTile - 1) / kDictTile);
+    for (uint64_t t = 0; t < tiles; ++t) {
+      g.push_back(jobs[j]);
+      g.back().tile_base = t;
+    }
+  }
+  if (g.empty()) return ORCG_OK;
+  if (g.size() > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many rows");
+  const void* d = nullptr;
+  const int rc = stage_table(ctx, g.data(), g.size() * sizeof(DictJob), &d);
+  if (rc) return rc;
+  out.push_back(MultiLaunch{2, 0, d, (uint32_t)g.size(), g.size(), 0});
+  return ORCG_OK;
+}
+
+int launch_dict_jobs(Ctx* ctx, const DictJob* d_jobs, uint32_t njobs, uint64_t tiles) {
+  hipLaunchKernelGGL(dict_multi_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_jobs, njobs);
+  return hip_check(ctx, hipGetLastError(), "dict_multi_kernel launch");
+}
+
+int launch_dict_multi(Ctx* ctx, const DictJob* jobs, uint32_t njobs) {
+  std::vector<MultiLaunch> ls;
+  const int rc = plan_dict_multi(ctx, jobs, njobs, ls);
+  return rc ? rc : run_multi(ctx, ls);
 }
 
 }  // namespace orcg

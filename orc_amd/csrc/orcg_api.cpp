@@ -209,6 +209,13 @@ void pinned_free(void* p) {
   }
 }
 
+void debug_stale(const char* where) {
+  static const bool on = getenv("ORCG_DEBUG_STALE") != nullptr;
+  if (!on) return;
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "orcg: pending HIP error at %s: %s\n", where, hipGetErrorString(e));
+}
+
 unsigned side_lanes() {
   static const unsigned n = [] {
     const char* e = getenv("ORCG_LANES");

@@ -53,11 +53,17 @@ struct Ctx {
   uint64_t defer_cap = 0;
   uint64_t defer_seq = 0;  // serial + drain launch pairs so far (their entries' stamps)
   int num_cus = 0;         // compute units of `device` (0 = not queried yet)
-  // job tables of multi-stream RLEv2 launches: a pinned host ring and its
-  // device mirror (launch_rlev2_multi)
+  // job tables of multi-stream launches: a pinned host ring and its device
+  // mirror, in bytes (stage_table)
   void* h_jobs = nullptr;
   void* d_jobs = nullptr;
   uint64_t jobs_cap = 0, jobs_used = 0;
+  // or an arena the caller uploads itself (the file reader's stripe staging):
+  // stage_table writes a table to arena_h and hands out arena_d; the caller
+  // orders the arena's upload before the launches (plan_* / run_multi)
+  uint8_t* arena_h = nullptr;
+  uint8_t* arena_d = nullptr;
+  uint64_t arena_cap = 0, arena_used = 0;
   // side contexts (own stream, scratch, queues) the file reader decodes
   // sibling column subtrees on concurrently, forked from and joined back into
   // this context's stream with events; created on first use (ctx_lane)
@@ -95,7 +101,24 @@ struct RleJob {
   const uint64_t* dcount;   // non-null: the value count on the device (nvalues is then the output's capacity)
 };
 
+// One RLEv1 segment of a multi-stream launch, built on the host from the
+// stream's plan or row index: a workgroup reads its whole description in one
+// load (no job search through the table on the device).
+struct V1SegDesc {
+  const uint8_t* src;
+  uint64_t src_len;
+  uint64_t seg_start, vi;  // first byte (a group header) and its first value
+  uint64_t seg_end, v_next;  // the next segment's, or (src_len, ~0) for the last
+  void* dst;               // int64 values [0, nvalues)
+  uint64_t nvalues;
+  unsigned long long* err;
+  uint32_t is_signed, pad;
+};
+
 int set_error(Ctx* ctx, int status, const std::string& msg);
+// ORCG_DEBUG_STALE=1: report (and clear) a HIP error left pending on this
+// host thread at `where` (launch checks read hipGetLastError).
+void debug_stale(const char* where);
 // page-locked host memory (transparent huge pages + hipHostRegister for large
 // buffers, hipHostMalloc otherwise); pinned_free takes either kind
 void* pinned_alloc(size_t bytes);
@@ -129,6 +152,28 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
 int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs);
 // Variants whose instances take job tables with row-index segments (RleJob::trip).
 bool rlev2_multi_capable(int variant);
+// Copies a job table into the context's arena (no copy enqueued) or its
+// pinned ring and device mirror (an H2D ordered on ctx->stream); *out = the
+// device copy.
+int stage_table(Ctx* ctx, const void* src, size_t bytes, const void** out);
+inline int stage_rle_jobs(Ctx* ctx, const RleJob* jobs, uint32_t n, const RleJob** out) {
+  return stage_table(ctx, jobs, (size_t)n * sizeof(RleJob), (const void**)out);
+}
+
+// A multi-stream launch planned ahead of the upload that carries its job
+// table (stage_table in arena mode): plan_* group, order and stage the
+// jobs; run_multi enqueues the kernels (RLEv2 instances on side lanes).
+struct MultiLaunch {
+  int kind;           // 0 RLEv2 instance `variant`, 1 RLEv1, 2 dictionaries
+  int variant;
+  const void* d_jobs;
+  uint32_t njobs;
+  uint64_t grid;      // segments / tiles
+  uint64_t values;
+};
+int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<MultiLaunch>& out);
+int plan_rlev1_multi(Ctx* ctx, const V1SegDesc* segs, uint64_t nsegs, std::vector<MultiLaunch>& out);
+int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& launches);
 
 // d_ones (boolean mode, may be null): += the set rows written (a PRESENT
 // stream's non-null rows), one atomic per wave. d_nout (may be null): the
@@ -138,6 +183,10 @@ int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint6
                    const uint64_t* d_nout = nullptr);
 int launch_rlev1(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed, const uint64_t* d_segtab,
                  uint64_t nsegs, uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes);
+// The segments of several RLEv1 streams (int64 output) in one launch per
+// chunk width (rlev1_kernel's narrow instance for short segments).
+int launch_rlev1_multi(Ctx* ctx, const V1SegDesc* segs, uint64_t nsegs);
+int launch_rlev1_jobs(Ctx* ctx, const V1SegDesc* d_segs, uint64_t nsegs, int chunk);
 int launch_scatter(Ctx* ctx, const void* d_dense, const uint8_t* d_nn, uint64_t n, void* d_out, int width,
                    int fill_mode, int64_t fill);
 // (d_summary, may be null: [0] blob bytes, [1] any negative length)
@@ -145,6 +194,26 @@ int launch_dict_offsets(Ctx* ctx, const int64_t* d_lengths, uint64_t dict_size, 
                         uint64_t* d_summary = nullptr);
 int launch_dict_gather(Ctx* ctx, const void* d_idx, int idx_width, const uint8_t* d_nn, uint64_t n,
                        const int64_t* d_offsets, uint64_t dict_size, int64_t* d_start, int64_t* d_len);
+// One dictionary column of a batched launch (dict_multi_kernel): entry
+// lengths -> offsets + {blob bytes, negative-length flag} summary, and the
+// bounds-checked gather of n rows (n = 0: offsets only, lazy decoding).
+constexpr uint32_t kDictLds = 4096;  // largest dictionary a batch takes
+struct DictJob {
+  const int64_t* lengths;
+  uint64_t dict_size;
+  int64_t* offsets;   // dict_size + 1
+  uint64_t* summary;  // [0] blob bytes, [1] any negative length
+  const int64_t* idx;
+  const uint8_t* nn;  // row not-null mask, or null
+  uint64_t n;
+  int64_t* start;
+  int64_t* len;
+  unsigned long long* err;
+  uint64_t tile_base;  // set by the launcher
+};
+int launch_dict_multi(Ctx* ctx, const DictJob* jobs, uint32_t njobs);
+int plan_dict_multi(Ctx* ctx, const DictJob* jobs, uint32_t njobs, std::vector<MultiLaunch>& out);
+int launch_dict_jobs(Ctx* ctx, const DictJob* d_jobs, uint32_t njobs, uint64_t tiles);
 
 // Varint decimals (decimal_kernels.hip): per-tile (kVarintTile bytes) terminator counts,
 // then (after an exclusive scan of the counts) the decode + rescale into

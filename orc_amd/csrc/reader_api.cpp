@@ -215,10 +215,13 @@ struct HostStage {
   uint64_t n_pos = 0, n_plan = 0;  // RLE streams cut by the row index / by a host plan
   uint64_t n_chunks = 0;            // compression chunks inflated (ReaderMetrics::DecompressionCall)
   uint64_t rows_off = 0;   // staging offset of int64 rows[g] = g * stride
+  // room kept past the prepared bytes for the upload's tail (read-back block
+  // and job arena, upload_tail_bytes): upload_and_decode never reallocates
+  uint64_t slack = 0;
   ~HostStage() { pinned_free(h); }
   bool ensure(uint64_t bytes, uint64_t keep) {
     if (bytes <= cap) return true;
-    const uint64_t ncap = std::max<uint64_t>(bytes + (bytes >> 2), 1 << 20);
+    const uint64_t ncap = std::max<uint64_t>(bytes + (bytes >> 2), 1 << 20) + slack;
     uint8_t* nh = (uint8_t*)pinned_alloc(ncap);
     if (!nh) return false;
     if (h) {
@@ -259,7 +262,10 @@ struct DevSlot {
   uint64_t stripe = ~0ull;
   DevPool pool;
   uint8_t* d_stage = nullptr;
-  uint64_t* d_scalars = nullptr;
+  // the read-back block, uploaded initialised with the stripe and copied
+  // back once after the decode: per column its error record, its PRESENT
+  // decode's non-null count, then the summary slots (rb_alloc)
+  uint64_t* d_rb = nullptr;
   unsigned long long* d_errs = nullptr;  // device error record per column (the kernels' atomicMin word)
   uint64_t* d_ones = nullptr;            // per column: non-null rows its PRESENT decode wrote
   std::vector<ColOut> out;
@@ -328,7 +334,22 @@ struct orcg_reader {
   static constexpr uint32_t kNoCol = 0xffffffffu;
   uint32_t cur_col = kNoCol, err_col = kNoCol;
   int first_error(int inline_rc);
+  // the read-back block's pinned mirror (valid after first_error's copy)
+  uint64_t* h_rb = nullptr;
+  size_t h_rb_cap = 0, rb_words = 0, rb_slot0 = 0, rb_used = 0;
+  // `count` words of the read-back block: the device address a kernel writes,
+  // and (*host) where the host reads it after the stripe's synchronisation
+  uint64_t* rb_alloc(size_t count, const uint64_t** host) {
+    if (!D->d_rb || rb_used + count > rb_words) return nullptr;
+    uint64_t* d = D->d_rb + rb_used;
+    *host = h_rb + rb_used;
+    rb_used += count;
+    return d;
+  }
   const uint64_t* defer(const void* d_src, size_t count) {
+    // a value in the read-back block rides its one copy
+    if (D && D->d_rb && (const uint64_t*)d_src >= D->d_rb && (const uint64_t*)d_src + count <= D->d_rb + rb_words)
+      return h_rb + ((const uint64_t*)d_src - D->d_rb);
     if (defer_used + count > defer_cap) return nullptr;
     uint64_t* h = h_defer + defer_used;
     defer_used += count;
@@ -366,6 +387,7 @@ struct orcg_reader {
     if (mapped) munmap(mapped, file_len);
     if (h_defer) (void)hipHostFree(h_defer);
     if (h_sync) (void)hipHostFree(h_sync);
+    if (h_rb) (void)hipHostFree(h_rb);
   }
   int fail(int status, const std::string& m) {
     if (err_col == kNoCol) err_col = cur_col;
@@ -402,6 +424,9 @@ struct orcg_reader {
   // not read back mid-stripe (one stream synchronisation per nullable column
   // saved); has_nulls is settled with the stripe's checks.
   bool device_counts(const Col& c) const;
+  // Whether decode(id) launches device work: false when everything it needs
+  // came from the stripe's batched launches (streams, dictionaries)
+  bool device_work(uint32_t id) const;
   // Side streams for sibling subtrees (ORCG_LANES, default 4; 1 = one
   // stream). in_lane: decode() runs on a side context (no nested forks).
   bool in_lane = false;
@@ -461,9 +486,23 @@ struct orcg_reader {
   // launch per kernel instance (launch_rlev2_multi); decode() then finds
   // their outputs here.
   bool batch_on = true;
-  std::vector<RleJob> batch;
+  std::vector<RleJob> batch;          // RLEv2 streams
+  std::vector<V1SegDesc> v1_segs;     // RLEv1 streams' segments
+  // dictionary columns of the batch (no nulls, <= kDictLds entries): their
+  // offsets and gathers in one launch after the streams (dict_multi_kernel)
+  struct DictDone {
+    int64_t* offsets;
+    const uint64_t* h_summary;
+    int64_t* start;
+    int64_t* len;
+    int64_t* idx;
+  };
+  std::vector<DictJob> dict_batch;
+  std::unordered_map<uint32_t, DictDone> dict_done;
+  std::vector<MultiLaunch> launches;
   std::unordered_map<uint64_t, std::pair<int64_t*, uint64_t>> batched;  // (column, slot) -> (values, count)
   int queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2);
+  int queue_dict(uint32_t id, uint64_t n);
   int collect(uint32_t id, uint64_t n, const int64_t* rg_rows);
   int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones = nullptr,
                   const uint64_t* d_count = nullptr);
@@ -578,6 +617,23 @@ bool orcg_reader::device_counts(const Col& c) const {
   return is_string_kind(k) && c.encoding == kDictionaryV2;
 }
 
+bool orcg_reader::device_work(uint32_t id) const {
+  const Col& c = H->cols[id];
+  if (!selected[id] || !c.supported) return false;
+  if (c.s[kSlotPresent].present) return true;
+  const uint32_t k = c.kind;
+  auto done = [&](int slot) { return !c.s[slot].present || batched.count((uint64_t)id * 8 + (uint64_t)slot) != 0; };
+  if (k == ORCG_TYPE_STRUCT) {
+    for (uint32_t st : footer.types[id].subtypes)
+      if (device_work(st)) return true;
+    return false;
+  }
+  if (is_int_kind(k)) return !done(kSlotData);
+  if (k == ORCG_TYPE_DOUBLE) return false;  // the stream bytes are the values
+  if (is_string_kind(k) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)) return dict_done.count(id) == 0;
+  return true;
+}
+
 int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** pout, bool force_v2,
                             const uint64_t* dcount) {
   const uint64_t key = (uint64_t)(&c - H->cols.data()) * 8 + (uint64_t)slot;
@@ -619,10 +675,47 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
   // left to decode(): empty or missing streams, RLEv1, a host plan short of
   // values (decode() raises the error in column order)
   if (count == 0 || !sb.present) return ORCG_OK;
-  if (!force_v2 && (c.encoding == kDirect || c.encoding == kDictionary)) return ORCG_OK;
+  const bool v1 = !force_v2 && (c.encoding == kDirect || c.encoding == kDictionary);
   if (!sb.pos && count > sb.plan->values) return ORCG_OK;
+  // (collect() runs before the stripe's upload: no device work here)
+  if (sb.pos && !(cur_rows && (v1 || rlev2_multi_capable(ctx->rlev2_variant)))) return ORCG_OK;
+  if (v1) {
+    // RLEv1: one host-built descriptor per segment (the plan's cuts, or the
+    // row index with the stripe's row-group starts g * stride)
+    int64_t* out = alloc<int64_t>(count);
+    if (!out) return fail_oom(__LINE__);
+    const uint8_t* d_src = D->d_stage + sb.host_off;
+    const uint64_t stride = footer.row_index_stride;
+    const size_t ns = sb.pos ? (size_t)H->ngroups : sb.plan->segs.size();
+    auto at = [&](size_t g, uint64_t* off) -> uint64_t {
+      if (sb.pos) {
+        *off = (uint64_t)sb.trip[3 * g];
+        const int64_t v = (int64_t)(g * stride) - sb.trip[3 * g + 1];
+        return v < 0 ? 0ull : (uint64_t)v;
+      }
+      *off = sb.plan->segs[g].byte_offset;
+      return sb.plan->segs[g].value_index;
+    };
+    for (size_t g = 0; g < ns; ++g) {
+      V1SegDesc d{};
+      d.src = d_src;
+      d.src_len = sb.len;
+      d.vi = at(g, &d.seg_start);
+      d.seg_end = sb.len;
+      d.v_next = ~0ull;
+      if (g + 1 < ns) d.v_next = at(g + 1, &d.seg_end);
+      d.dst = out;
+      d.nvalues = count;
+      d.err = D->d_errs + id;
+      d.is_signed = is_signed ? 1u : 0u;
+      v1_segs.push_back(d);
+    }
+    ++metrics[4];  // DecodingCall
+    batched[(uint64_t)id * 8 + (uint64_t)slot] = {out, count};
+    return ORCG_OK;
+  }
   RleJob j{};
-  if (sb.pos && cur_rows && rlev2_multi_capable(ctx->rlev2_variant)) {
+  if (sb.pos) {
     // the row index is the segment table (no rg_segtab launch): collect()
     // only queues columns whose rows are all values (no mask)
     j.trip = (const int64_t*)(D->d_stage + sb.rg_off);
@@ -650,6 +743,37 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
   return ORCG_OK;
 }
 
+// A dictionary column whose streams are both batched: its offsets and row
+// gather join the stripe's dictionary launch (decode() then only wires the
+// outputs and registers its checks).
+int orcg_reader::queue_dict(uint32_t id, uint64_t n) {
+  Col& c = H->cols[id];
+  const uint64_t D_ = c.dict_size;
+  if (D_ > kDictLds || !c.s[kSlotData].present) return ORCG_OK;
+  if (D_ > 0 && !c.s[kSlotLength].present) return ORCG_OK;  // decode() raises the missing stream
+  const auto li = batched.find((uint64_t)id * 8 + kSlotLength);
+  const auto di = batched.find((uint64_t)id * 8 + kSlotData);
+  if ((D_ > 0 && li == batched.end()) || (n > 0 && di == batched.end())) return ORCG_OK;
+  DictJob j{};
+  j.lengths = D_ ? li->second.first : nullptr;
+  j.dict_size = D_;
+  ORCG_ALLOC_TO(int64_t, j.offsets, D_ + 1);
+  const uint64_t* h_summary = nullptr;
+  j.summary = rb_alloc(2, &h_summary);
+  if (!j.summary) return ORCG_OK;
+  j.idx = n ? di->second.first : nullptr;
+  j.nn = nullptr;
+  j.n = lazy_dict ? 0 : n;
+  if (!lazy_dict) {
+    ORCG_ALLOC_TO(int64_t, j.start, n);
+    ORCG_ALLOC_TO(int64_t, j.len, n);
+  }
+  j.err = D->d_errs + id;
+  dict_batch.push_back(j);
+  dict_done[id] = DictDone{j.offsets, h_summary, j.start, j.len, const_cast<int64_t*>(j.idx)};
+  return ORCG_OK;
+}
+
 // The streams decode() will read with host-known counts, in its order
 // (same slots, signedness and counts as decode()'s int_stream calls).
 int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
@@ -674,6 +798,7 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
     if (c.encoding == kDictionary || c.encoding == kDictionaryV2) {
       rc = queue_stream(id, kSlotLength, false, c.dict_size, false);
       if (!rc) rc = queue_stream(id, kSlotData, false, n, false);
+      if (!rc) rc = queue_dict(id, n);
     } else {
       rc = queue_stream(id, kSlotLength, false, n, false);
     }
@@ -864,8 +989,13 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
           ORCG_ALLOC_TO(uint8_t, rnn, n + 8);
           if ((rc = scatter(keep, row_nn, n, rnn, 1))) return fail_ctx(rc);
         }
-        if ((rc = launch_count_nonzero(ctx, rnn, n, D->d_scalars + 3))) return fail_ctx(rc);
-        const uint64_t* kept = defer(D->d_scalars + 3, 1);
+        // the column's own count word: sibling decimal columns decode on
+        // other side lanes concurrently
+        const uint64_t* h_kept = nullptr;
+        uint64_t* kept_d = rb_alloc(1, &h_kept);
+        if (!kept_d) ORCG_ALLOC_TO(uint64_t, kept_d, 1);
+        if ((rc = launch_count_nonzero(ctx, rnn, n, kept_d))) return fail_ctx(rc);
+        const uint64_t* kept = defer(kept_d, 1);
         if (!kept) return fail(ORCG_DEVICE_ERROR, "D2H of the kept decimal count failed");
         Col* cp = &c;
         checks.emplace_back(cur_col, [cp, kept, rnn, n]() -> int {
@@ -924,11 +1054,34 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     const bool dict = c.encoding == kDictionary || c.encoding == kDictionaryV2;
     int64_t* start = nullptr;
     int64_t* len = nullptr;
-    if (!(dict && lazy_dict)) {
+    if (!(dict && lazy_dict) && !(dict && dict_done.count(id))) {
       ORCG_ALLOC_TO(int64_t, start, n);
       ORCG_ALLOC_TO(int64_t, len, n);
     }
-    if (dict) {
+    const auto dd = dict ? dict_done.find(id) : dict_done.end();
+    if (dd != dict_done.end()) {
+      // batched (queue_dict): offsets, summary and gather come from the
+      // stripe's dictionary launch; the reference's checks, in its order
+      const std::string cid = std::to_string(id);
+      const uint64_t* h = dd->second.h_summary;
+      StreamBuf& db = c.s[kSlotDict];
+      Col* cp = &c;
+      const bool db_present = db.present;
+      const uint64_t db_len = db.present ? db.len : 0;
+      checks.emplace_back(cur_col, [this, h, cp, db_present, db_len, cid]() -> int {
+        if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
+        if (h[0] > 0 && !db_present)
+          return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
+        if (h[0] > db_len) return fail(ORCG_PARSE_ERROR, "bad read in readFully");
+        cp->blob_len = h[0];
+        return ORCG_OK;
+      });
+      c.blob = db.present ? D->d_stage + db.host_off : nullptr;
+      c.index = dd->second.idx;
+      c.dict_offsets = dd->second.offsets;
+      start = dd->second.start;
+      len = dd->second.len;
+    } else if (dict) {
       // loadStringDictionary (DictionaryLoader.cc:43-97), then
       // StringDictionaryColumnReader::next (ColumnReader.cc:561-594)
       const uint64_t dict_size = c.dict_size;
@@ -938,7 +1091,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       int64_t* dlen;
       ORCG_ALLOC(int64_t, doff, dict_size + 1);
       if ((rc = int_stream(c, kSlotLength, false, dict_size, &dlen))) return rc;
-      ORCG_ALLOC(uint64_t, summary, 2);  // blob bytes, negative-length flag
+      const uint64_t* h_sum = nullptr;
+      uint64_t* summary = rb_alloc(2, &h_sum);  // blob bytes, negative-length flag
+      if (!summary) ORCG_ALLOC_TO(uint64_t, summary, 2);
       if (dict_size <= 65536) {
         // offsets, blob size and the negative-length check in one launch
         if ((rc = launch_dict_offsets(ctx, dlen, dict_size, doff, summary))) return fail_ctx(rc);
@@ -1042,9 +1197,14 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if ((rc = decode(st, total, nullptr, total, child_rows))) return rc;
   } else if (k == ORCG_TYPE_STRUCT) {
     std::vector<uint32_t> kids;
+    size_t busy = 0;  // subtrees with launches of their own (the rest only wire batched outputs)
     for (uint32_t st : footer.types[id].subtypes)
-      if (selected[st] && H->cols[st].supported) kids.push_back(st);
-    const unsigned nl = in_lane ? 1u : (unsigned)std::min<size_t>(num_lanes(), kids.size());
+      if (selected[st] && H->cols[st].supported) {
+        kids.push_back(st);
+        busy += device_work(st) ? 1 : 0;
+      }
+    // side streams only pay when at least two subtrees launch work
+    const unsigned nl = in_lane || busy < 2 ? 1u : (unsigned)std::min<size_t>(num_lanes(), kids.size());
     if (nl <= 1) {
       for (uint32_t st : kids)
         if ((rc = decode(st, n, c.nn, nonnull, rg_rows, c.nn ? d_nonnull : nullptr, &c))) return rc;
@@ -1183,6 +1343,29 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   return ORCG_OK;
 }
 
+// What upload_and_decode appends to a stripe's staging for nc columns: the
+// read-back block (error records, non-null counts, summary slots) and the
+// job arena of the batched launches, each 256-byte aligned.
+static uint64_t rb_words_for(size_t nc) { return 2 * nc + 1 + 4 * nc + 16; }
+static uint64_t arena_bytes_for(size_t nc, uint64_t v1_segs, uint64_t dict_tiles) {
+  // (dictionary jobs: one copy per 2,048-row tile of a column)
+  return 5 * (nc + 1) * sizeof(RleJob) + (nc + 1) * sizeof(DictJob) * dict_tiles + v1_segs * sizeof(V1SegDesc) +
+         16 * 256;
+}
+static uint64_t upload_tail_bytes(size_t nc, uint64_t v1_segs, uint64_t dict_tiles) {
+  return 256 + 8 * rb_words_for(nc) + 256 + arena_bytes_for(nc, v1_segs, dict_tiles) + 64;
+}
+// RLEv1 segments of a prepared stripe (each a descriptor in the arena)
+static uint64_t v1_segments(const HostStage& hs) {
+  uint64_t n = 0;
+  for (const Col& c : hs.cols) {
+    if (c.encoding != kDirect && c.encoding != kDictionary) continue;
+    for (const StreamBuf& sb : c.s)
+      if (sb.present) n += sb.pos ? hs.ngroups : (sb.plan ? sb.plan->segs.size() : 0);
+  }
+  return n;
+}
+
 // Host half of a stripe read (thread-safe w.r.t. the device half of another
 // stripe): stripe footer (Reader.cc getStripeFooter :620-640), stream
 // location (StripeStream.cc:82-125), decompression of every selected stream
@@ -1199,6 +1382,9 @@ static uint64_t small_stream_bytes() {
   const char* e = getenv("ORCG_SMALL_STREAM");
   return e ? strtoull(e, nullptr, 10) : 0;
 }
+
+// RLEv1 streams up to this size decode in 1 KB host-plan segments
+constexpr uint64_t kV1SmallStream = 64u << 10;
 
 static bool fine_plans() {
   static const bool on = [] {
@@ -1249,6 +1435,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     return hs.fail(ORCG_PARSE_ERROR, "bad number of ColumnEncodings in StripeFooter: expected=" +
                                          std::to_string(nt) + ", actual=" + std::to_string(sf.encodings.size()));
   hs.cols = std::vector<Col>(nt);
+  hs.slack = upload_tail_bytes(nt, 0, (si.num_rows + 2047) / 2048 + 1);
   for (size_t i = 0; i < nt; ++i) {
     hs.cols[i].kind = footer.types[i].kind;
     hs.cols[i].encoding = sf.encodings[i].kind;
@@ -1493,6 +1680,11 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
         const uint64_t per_group = hs.ngroups ? sb.len / hs.ngroups : 0;
         if (sb.len <= small) {
           // small stream: a host plan (small_stream_bytes)
+        } else if (kind == 1 && sb.len <= kV1SmallStream) {
+          // a small RLEv1 stream (configs[0]: 5,000-row stripes, <= 5 KB
+          // streams, one row group): 1 KB host-plan segments instead of one
+          // row-group segment, so the stream's windows decode side by side
+          // (rlev1_kernel's narrow instance) -- the host walk is ~1 ns a byte
         } else if (kind == 0) {
           if (per_group <= (2u << 10)) continue;
         } else if (kind == 2 && fine_plans() && c.s[kSlotPresent].present && per_group > (8u << 10) &&
@@ -1515,7 +1707,8 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     const uint8_t* p = hs.h + sb.host_off;
     // byte / boolean RLE without row-index segments: 1 KB segments (one wave each: enough waves to fill the GPU)
     if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, 1u << 10, 1024));
-    else if (rle_kind[q] == 1) sb.plan.reset(make_v1_plan(p, sb.len, 16u << 10, 8192));
+    else if (rle_kind[q] == 1)
+      sb.plan.reset(make_v1_plan(p, sb.len, sb.len <= kV1SmallStream ? (1u << 10) : (16u << 10), 8192));
     else if (rle_kind[q] == 3) sb.plan.reset(make_plan(p, sb.len, 8u << 10, 4096));
     else sb.plan.reset(make_plan(p, sb.len, 16u << 10, 8192));
   }, plan_bytes, 512u << 10);  // header walks: ~512 KB of stream per thread
@@ -1524,6 +1717,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
   hs.n_pos = 0;
   for (auto& c : hs.cols)
     for (auto& sb : c.s) hs.n_pos += sb.pos ? 1 : 0;
+  hs.slack = upload_tail_bytes(nt, v1_segments(hs), (si.num_rows + 2047) / 2048 + 1);
   uint64_t seg_bytes = 0;
   for (auto* sb : rle) seg_bytes += ((sb->plan->segs.size() * sizeof(orcg_segment)) + 255) & ~(uint64_t)255;
   w = (w + 255) & ~(uint64_t)255;
@@ -1570,11 +1764,13 @@ int orcg_reader::first_error(int inline_rc) {
   const std::string inline_msg = last_error;
   const uint32_t inline_col = err_col;
   cur_col = kNoCol;
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(ORCG_DEVICE_ERROR, "stream synchronize failed");
+  // one copy brings back the error records, the non-null counts and the
+  // summary slots (rb_alloc), then one synchronisation
   const size_t nc = H->cols.size();
-  std::vector<unsigned long long> rec(nc, kNoError);
-  if (nc && hipMemcpy(rec.data(), D->d_errs, 8 * nc, hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpyAsync(h_rb, D->d_rb, 8 * rb_used, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
     return fail(ORCG_DEVICE_ERROR, "read error records");
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(ORCG_DEVICE_ERROR, "stream synchronize failed");
+  std::vector<unsigned long long> rec(h_rb, h_rb + nc);
   const uint32_t last = inline_rc ? (inline_col == kNoCol ? 0u : inline_col) : (uint32_t)nc;
   // checks grouped by column once (stable: a column's checks keep their
   // order), then one walk over columns and checks together
@@ -1605,34 +1801,72 @@ int orcg_reader::first_error(int inline_rc) {
       const int rc = ch.second();
       if (rc) return rc;
     }
-  const int rc = sync_ctx(ctx);
-  return rc ? fail_ctx(rc) : ORCG_OK;
+  // the context's own record (launches outside a column's scope)
+  const unsigned long long own = h_rb[2 * nc];
+  if (own != kNoError) {
+    const uint32_t code = (uint32_t)(own & 0xff);
+    ctx->last_error_value = own >> 8;
+    return fail(dev_error_status(code), dev_error_message(code));
+  }
+  return ORCG_OK;
 }
 
 // Device half: one H2D of the staging buffer, then every selected column.
 int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   const double t0 = now_s();
+  // Launch checks read hipGetLastError (per host thread): drop a failure a
+  // call whose result was already checked or deliberately ignored (frees in
+  // destructors, a retried allocation) left behind, so it cannot surface as
+  // this stripe's first launch error.
+  {
+    const hipError_t stale = hipGetLastError();
+    static const bool dbg = getenv("ORCG_DEBUG_STALE") != nullptr;
+    if (dbg && stale != hipSuccess) fprintf(stderr, "orcg: stale HIP error before upload: %s\n", hipGetErrorString(stale));
+  }
   ds.stripe = hs.stripe;
   ds.pool.release_all();
-  ds.d_stage = (uint8_t*)ds.pool.get(hs.used + 64);
-  ds.d_scalars = (uint64_t*)ds.pool.get(64);
-  ds.d_errs = (unsigned long long*)ds.pool.get(8 * hs.cols.size() + 8);
-  ds.d_ones = (uint64_t*)ds.pool.get(8 * hs.cols.size() + 8);
-  if (!ds.d_stage || !ds.d_scalars || !ds.d_errs || !ds.d_ones) return fail_oom(__LINE__);
-  stage_bytes += hs.used;
-  int rc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, hs.used, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
-  if (!rc) rc = hip_check(ctx, hipMemsetAsync(ds.d_errs, 0xff, 8 * hs.cols.size(), ctx->stream), "error records");
-  if (!rc) rc = hip_check(ctx, hipMemsetAsync(ds.d_ones, 0, 8 * hs.cols.size(), ctx->stream), "row counts");
-  // The decode's launches follow the copy on the same stream (side lanes
-  // wait on a fork event recorded after it): the synchronisation only splits
-  // the H2D phase out of the timings, so small stripes (configs[0]: ~50 KB of
-  // staging) skip it and count their copy in the decode phase.
-  if (!rc && hs.used >= (1u << 20)) rc = sync_ctx(ctx);
-  if (rc) return fail_ctx(rc);
-  const double t1 = now_s();
+  const size_t nc = hs.cols.size();
+  const uint64_t nrows_stripe = footer.stripes[hs.stripe].num_rows;
+  // after the streams: the read-back block (error records 0xff.., non-null
+  // counts and summary slots 0) and the job arena (the batched launches'
+  // tables): one upload carries the stripe, its initialised counters and
+  // its job tables
+  const uint64_t rb_off = (hs.used + 255) & ~(uint64_t)255;
+  rb_words = rb_words_for(nc);
+  rb_slot0 = rb_used = 2 * nc + 1;  // word 2 nc: the context's own record during this stripe
+  const uint64_t arena_off = (rb_off + 8 * rb_words + 255) & ~(uint64_t)255;
+  const uint64_t arena_cap = arena_bytes_for(nc, v1_segments(hs), (nrows_stripe + 2047) / 2048 + 1);
+  const uint64_t total = arena_off + arena_cap;
+  if (!hs.ensure(total + 64, hs.used)) return fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
+  memset(hs.h + rb_off, 0xff, 8 * nc);
+  memset(hs.h + rb_off + 8 * nc, 0, 8 * (rb_words - nc));
+  memset(hs.h + rb_off + 8 * (2 * nc), 0xff, 8);
+  debug_stale("upload: staging ensured");
+  ds.d_stage = (uint8_t*)ds.pool.get(total + 64);
+  if (!ds.d_stage) return fail_oom(__LINE__);
+  debug_stale("upload: device slot");
+  ds.d_rb = (uint64_t*)(ds.d_stage + rb_off);
+  ds.d_errs = (unsigned long long*)ds.d_rb;
+  ds.d_ones = ds.d_rb + nc;
+  if (h_rb_cap < rb_words) {
+    if (h_rb) (void)hipHostFree(h_rb);
+    h_rb = nullptr;
+    h_rb_cap = 0;
+    if (hipHostMalloc((void**)&h_rb, rb_words * 8, hipHostMallocDefault) != hipSuccess)
+      return fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed");
+    h_rb_cap = rb_words;
+  }
   H = &hs;
   D = &ds;
-  const size_t need_defer = 4 * hs.cols.size() + 16;
+  // the context's own record for this stripe rides the read-back block (the
+  // stripe's one copy back replaces sync_ctx's synchronous record read)
+  struct OwnRecord {
+    Ctx* c;
+    unsigned long long* saved;
+    ~OwnRecord() { c->d_err = saved; }
+  } own_rec{ctx, ctx->d_err};
+  ctx->d_err = (unsigned long long*)(ds.d_rb + 2 * nc);
+  const size_t need_defer = 4 * nc + 16;
   if (defer_cap < need_defer) {
     if (h_defer) (void)hipHostFree(h_defer);
     h_defer = nullptr;
@@ -1645,18 +1879,49 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   checks.clear();
   cur_col = err_col = kNoCol;
   batch.clear();
+  v1_segs.clear();
   batched.clear();
+  dict_batch.clear();
+  dict_done.clear();
+  launches.clear();
   const uint64_t nrows = footer.stripes[hs.stripe].num_rows;
   const int64_t* rg_rows = hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr;
+  // the batch: streams (and dictionaries) whose counts the host knows, their
+  // job tables staged into the arena before the upload
+  int rc = ORCG_OK;
   if (batch_on) {
+    ctx->arena_h = hs.h + arena_off;
+    ctx->arena_d = ds.d_stage + arena_off;
+    ctx->arena_cap = arena_cap;
+    ctx->arena_used = 0;
     rc = collect(0, nrows, rg_rows);
-    if (!rc && !batch.empty()) {
-      rc = launch_rlev2_multi(ctx, batch.data(), (uint32_t)batch.size());
-      if (rc) rc = fail_ctx(rc);
-    }
+    if (!rc && !batch.empty() && (rc = plan_rlev2_multi(ctx, batch.data(), (uint32_t)batch.size(), launches)))
+      rc = fail_ctx(rc);
+    if (!rc && !v1_segs.empty() && (rc = plan_rlev1_multi(ctx, v1_segs.data(), v1_segs.size(), launches)))
+      rc = fail_ctx(rc);
+    if (!rc && !dict_batch.empty() &&
+        (rc = plan_dict_multi(ctx, dict_batch.data(), (uint32_t)dict_batch.size(), launches)))
+      rc = fail_ctx(rc);
+    ctx->arena_h = ctx->arena_d = nullptr;
+    ctx->arena_cap = 0;
   }
+  debug_stale("upload: batch planned");
+  const uint64_t up = arena_off + ctx->arena_used;
+  stage_bytes += up;
+  // (uploaded even after a failure above: first_error reads the records back)
+  const int urc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, up, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
+  if (urc && !rc) rc = fail_ctx(urc);
+  // The decode's launches follow the copy on the same stream (side lanes
+  // wait on a fork event recorded after it): the synchronisation only splits
+  // the H2D phase out of the timings, so small stripes (configs[0]: ~50 KB of
+  // staging) skip it and count their copy in the decode phase.
+  if (!rc && hs.used >= (1u << 20) && (rc = sync_ctx(ctx))) rc = fail_ctx(rc);
+  const double t1 = now_s();
+  debug_stale("upload: copied");
+  if (!rc && !launches.empty() && (rc = run_multi(ctx, launches))) rc = fail_ctx(rc);
   if (!rc) rc = decode(0, nrows, nullptr, nrows, rg_rows);
-  batched_streams += batch.size();
+  batched_streams += batched.size();
+  (void)arena_off;
   // queued copies land before the buffer is reused; then the first error in
   // column order, as the reference raises them one column at a time
   rc = first_error(rc);
@@ -1702,8 +1967,12 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   return rc;
 }
 
-// Stripes [first, first + count): the host prepares stripe i + 1 on a
-// worker thread while the GPU decodes stripe i.
+// Stripes [first, first + count): one host thread prepares stripe i + 1
+// (decompression, plans) while the caller's thread uploads and decodes stripe
+// i; the two stages alternate (stripe i in stages[i & 1]), so the preparer
+// waits only for the decode of stripe i - 1 to release its stage. One thread
+// for the whole read: a thread per stripe cost more than a configs[0] stripe
+// decodes in.
 int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   if (!ctx) return fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
   if (first > footer.stripes.size() || count > footer.stripes.size() - first)
@@ -1716,33 +1985,57 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   while (slots.size() < count) slots.emplace_back(new DevSlot());
   nslots = 0;
   if (count == 0) return ORCG_OK;
-  int rc = prepare(first, stages[0]);
-  timings[0] += stages[0].t_parse;
-  timings[1] += stages[0].t_decomp;
-  timings[2] += stages[0].t_plan;
-  stream_stats[0] += stages[0].n_pos;
-  stream_stats[1] += stages[0].n_plan;
-  if (rc) return fail(rc, stages[0].err);
-  for (uint64_t k = 0; k < count; ++k) {
-    HostStage& cur = stages[k & 1];
-    HostStage& nxt = stages[(k + 1) & 1];
-    std::thread worker;
-    const bool more = k + 1 < count;
-    if (more) worker = std::thread([&, k] { prepare(first + k + 1, nxt); });
-    rc = upload_and_decode(cur, *slots[k]);
-    if (more) worker.join();
-    if (rc) return rc;
-    nslots = k + 1;
-    if (more) {
-      timings[0] += nxt.t_parse;
-      timings[1] += nxt.t_decomp;
-      timings[2] += nxt.t_plan;
-      stream_stats[0] += nxt.n_pos;
-      stream_stats[1] += nxt.n_plan;
-      if (nxt.rc) return fail(nxt.rc, nxt.err);
+  std::mutex pm;
+  std::condition_variable pcv;
+  uint64_t prepared = 0, released = 0;  // stripes prepared; stripes whose stage the decode is done with
+  bool quit = false;
+  std::thread prep([&] {
+    for (uint64_t k = 0; k < count; ++k) {
+      {
+        std::unique_lock<std::mutex> lk(pm);
+        pcv.wait(lk, [&] { return quit || k < released + 2; });  // stripe k - 2 released stages[k & 1]
+        if (quit) return;
+      }
+      prepare(first + k, stages[k & 1]);
+      {
+        std::lock_guard<std::mutex> lk(pm);
+        prepared = k + 1;
+      }
+      pcv.notify_all();
+      if (stages[k & 1].rc) return;  // the decode raises it when it reaches stripe k
     }
+  });
+  int rc = ORCG_OK;
+  for (uint64_t k = 0; k < count && !rc; ++k) {
+    {
+      std::unique_lock<std::mutex> lk(pm);
+      pcv.wait(lk, [&] { return prepared > k; });
+    }
+    HostStage& cur = stages[k & 1];
+    timings[0] += cur.t_parse;
+    timings[1] += cur.t_decomp;
+    timings[2] += cur.t_plan;
+    stream_stats[0] += cur.n_pos;
+    stream_stats[1] += cur.n_plan;
+    if (cur.rc) {
+      rc = fail(cur.rc, cur.err);
+      break;
+    }
+    rc = upload_and_decode(cur, *slots[k]);
+    if (!rc) nslots = k + 1;
+    {
+      std::lock_guard<std::mutex> lk(pm);
+      released = k + 1;
+    }
+    pcv.notify_all();
   }
-  return ORCG_OK;
+  {
+    std::lock_guard<std::mutex> lk(pm);
+    quit = true;
+  }
+  pcv.notify_all();
+  prep.join();
+  return rc;
 }
 
 // ---- RowReader: batches of at most `capacity` rows over the stripes of a

@@ -2361,51 +2361,53 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
                       value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count);
 }
 
-// Job tables go through a pinned ring mirrored on the device: entries are
-// reused only after the stream has drained (a wrap synchronises first).
-static int stage_jobs(Ctx* ctx, const RleJob* jobs, uint32_t n, const RleJob** out) {
-  if (ctx->jobs_cap < n) {
+// Job tables go through a pinned ring mirrored on the device (entries are
+// reused only after the stream has drained: a wrap synchronises first), or
+// into the caller's arena (Ctx::arena_*), which the caller uploads itself.
+int stage_table(Ctx* ctx, const void* src, size_t bytes, const void** out) {
+  const uint64_t need = (bytes + 255) & ~(uint64_t)255;
+  if (ctx->arena_h) {
+    if (ctx->arena_used + need > ctx->arena_cap) return set_error(ctx, ORCG_INVALID_ARGUMENT, "job arena full");
+    memcpy(ctx->arena_h + ctx->arena_used, src, bytes);
+    *out = ctx->arena_d + ctx->arena_used;
+    ctx->arena_used += need;
+    return ORCG_OK;
+  }
+  if (ctx->jobs_cap < need) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->d_jobs) (void)hipFree(ctx->d_jobs);
     if (ctx->h_jobs) (void)hipHostFree(ctx->h_jobs);
     ctx->d_jobs = ctx->h_jobs = nullptr;
     ctx->jobs_cap = ctx->jobs_used = 0;
-    const uint64_t cap = std::max<uint64_t>(4 * (uint64_t)n, 1024);
-    int rc = hip_check(ctx, hipMalloc(&ctx->d_jobs, cap * sizeof(RleJob)), "hipMalloc job table");
-    if (!rc) rc = hip_check(ctx, hipHostMalloc(&ctx->h_jobs, cap * sizeof(RleJob), hipHostMallocDefault),
-                            "hipHostMalloc job table");
+    const uint64_t cap = std::max<uint64_t>(4 * need, 256u << 10);
+    int rc = hip_check(ctx, hipMalloc(&ctx->d_jobs, cap), "hipMalloc job table");
+    if (!rc) rc = hip_check(ctx, hipHostMalloc(&ctx->h_jobs, cap, hipHostMallocDefault), "hipHostMalloc job table");
     if (rc) return rc;
     ctx->jobs_cap = cap;
   }
-  if (ctx->jobs_used + n > ctx->jobs_cap) {
+  if (ctx->jobs_used + need > ctx->jobs_cap) {
     int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "job ring wrap");
     if (rc) return rc;
     ctx->jobs_used = 0;
   }
-  RleJob* h = (RleJob*)ctx->h_jobs + ctx->jobs_used;
-  RleJob* d = (RleJob*)ctx->d_jobs + ctx->jobs_used;
-  memcpy(h, jobs, n * sizeof(RleJob));
-  ctx->jobs_used += n;
+  uint8_t* h = (uint8_t*)ctx->h_jobs + ctx->jobs_used;
+  uint8_t* d = (uint8_t*)ctx->d_jobs + ctx->jobs_used;
+  memcpy(h, src, bytes);
+  ctx->jobs_used += need;
   *out = d;
-  return hip_check(ctx, hipMemcpyAsync(d, h, n * sizeof(RleJob), hipMemcpyHostToDevice, ctx->stream), "H2D jobs");
+  return hip_check(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream), "H2D jobs");
 }
 
 bool rlev2_multi_capable(int variant) { return variant == 0 || (variant >= 2 && variant <= 7); }
 
-int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
+int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<MultiLaunch>& out) {
   const int pinned = ctx->rlev2_variant;
   if (!rlev2_multi_capable(pinned)) {
     // not a multi-stream instance: one launch per stream (the reader queues
     // only segment-table jobs for these variants, rlev2_multi_capable)
     for (uint32_t j = 0; j < njobs; ++j) {
-      const RleJob& J = jobs[j];
-      if (!J.segtab) return set_error(ctx, ORCG_INVALID_ARGUMENT, "row-index job needs a multi-stream instance");
-      unsigned long long* const saved = ctx->d_err;  // the job's own error record
-      if (J.err) ctx->d_err = J.err;
-      int rc = launch_rlev2(ctx, J.src, J.src_len, (int)J.is_signed, J.segtab, J.nsegs, false, 0, 0, J.nvalues,
-                            J.dst, 8);
-      ctx->d_err = saved;
-      if (rc) return rc;
+      if (!jobs[j].segtab) return set_error(ctx, ORCG_INVALID_ARGUMENT, "row-index job needs a multi-stream instance");
+      out.push_back(MultiLaunch{3, pinned, jobs + j, 1, jobs[j].nsegs, jobs[j].nvalues});
     }
     return ORCG_OK;
   }
@@ -2423,26 +2425,9 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
         fprintf(stderr, "rle job: instance %d bytes %llu values %llu segments %llu (%.3f B/value)\n", v,
                 (unsigned long long)J.src_len, (unsigned long long)J.nvalues, (unsigned long long)J.nsegs,
                 (double)J.src_len / (double)J.nvalues);
-  // the instances' launches run concurrently on side streams (each is a few
-  // hundred to a couple of thousand workgroups of serial walks: together
-  // they fill the chip better than one after the other)
-  int ninst = 0;
-  for (int v = 2; v <= 7; ++v) ninst += group[v].empty() ? 0 : 1;
-  const bool par = ninst > 1 && side_lanes() > 1 && ctx_lane(ctx, (size_t)ninst - 1) != nullptr;
-  if (par) {
-    const int rc = hip_check(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork event");
-    if (rc) return rc;
-  }
-  Ctx* const base = ctx;
-  int li = 0;
   for (int v = 2; v <= 7; ++v) {
     std::vector<RleJob>& g = group[v];
     if (g.empty()) continue;
-    if (par) {
-      ctx = base->lanes[li++];
-      const int rc = hip_check(base, hipStreamWaitEvent(ctx->stream, base->ev_fork, 0), "fork wait");
-      if (rc) return rc;
-    }
     // workgroups start in index order: the streams with the most stream
     // bytes per value (the most runs per segment, the slowest segments) first,
     // so the launch does not end on a tail of slow segments
@@ -2457,27 +2442,85 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
     }
     if (segs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
     const RleJob* d = nullptr;
-    int rc = stage_jobs(ctx, g.data(), (uint32_t)g.size(), &d);
-    if (!rc) rc = launch_tiled(ctx, v, nullptr, 0, 0, nullptr, segs, false, 0, 0, values, nullptr, 8, d,
-                               (uint32_t)g.size());
-    if (rc) {
-      if (ctx != base) base->last_error = ctx->last_error;
-      ctx = base;
-      if (par)  // still join what was forked
-        for (int k = 0; k < li; ++k) {
-          (void)hipEventRecord(base->ev_join[k], base->lanes[k]->stream);
-          (void)hipStreamWaitEvent(base->stream, base->ev_join[k], 0);
-        }
-      return rc;
-    }
-  }
-  ctx = base;
-  for (int k = 0; par && k < li; ++k) {
-    int rc = hip_check(ctx, hipEventRecord(ctx->ev_join[k], ctx->lanes[k]->stream), "join event");
-    if (!rc) rc = hip_check(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_join[k], 0), "join wait");
+    const int rc = stage_rle_jobs(ctx, g.data(), (uint32_t)g.size(), &d);
     if (rc) return rc;
+    out.push_back(MultiLaunch{0, v, d, (uint32_t)g.size(), segs, values});
   }
   return ORCG_OK;
+}
+
+// The planned launches, in order; RLEv2 instances (kind 0) run concurrently
+// on side streams when there are several (each is a few hundred to a couple
+// of thousand workgroups of serial walks: together they fill the chip better
+// than one after the other), joined back before anything later.
+int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
+  int ninst = 0;
+  for (const MultiLaunch& m : ls) ninst += m.kind == 0 ? 1 : 0;
+  const bool par = ninst > 1 && side_lanes() > 1 && ctx_lane(ctx, (size_t)ninst - 1) != nullptr;
+  Ctx* const base = ctx;
+  int li = 0, rc = ORCG_OK;
+  if (par) rc = hip_check(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork event");
+  // the streams first (RLEv2 instances forked, RLEv1 on this stream
+  // meanwhile), then the join, then what reads their outputs (dictionaries)
+  bool joined = false;
+  auto join = [&]() -> int {
+    int r = ORCG_OK;
+    for (int k = 0; par && k < li; ++k) {
+      int jr = hip_check(base, hipEventRecord(base->ev_join[k], base->lanes[k]->stream), "join event");
+      if (!jr) jr = hip_check(base, hipStreamWaitEvent(base->stream, base->ev_join[k], 0), "join wait");
+      if (jr && !r) r = jr;
+    }
+    joined = true;
+    return r;
+  };
+  for (const MultiLaunch& m : ls) {
+    if (rc) break;
+    if (m.kind == 2 && !joined && (rc = join())) break;
+    debug_stale("run_multi: before a launch");
+    if (m.kind == 0) {
+      Ctx* c = base;
+      if (par) {
+        c = base->lanes[li++];
+        rc = hip_check(base, hipStreamWaitEvent(c->stream, base->ev_fork, 0), "fork wait");
+        if (rc) break;
+      }
+      // jobs without a record of their own report into the base's (the
+      // lane's own record is the lane's: it frees it)
+      unsigned long long* const own = c->d_err;
+      c->d_err = base->d_err;
+      rc = launch_tiled(c, m.variant, nullptr, 0, 0, nullptr, m.grid, false, 0, 0, m.values, nullptr, 8,
+                        (const RleJob*)m.d_jobs, m.njobs);
+      c->d_err = own;
+      if (rc) {
+        char b[160];
+        snprintf(b, sizeof b, " (instance %d, %u streams, %llu segments, lane %d)", m.variant, m.njobs,
+                 (unsigned long long)m.grid, par ? li - 1 : -1);
+        base->last_error = c->last_error + b;
+      }
+    } else if (m.kind == 1) {
+      rc = launch_rlev1_jobs(base, (const V1SegDesc*)m.d_jobs, m.grid, m.variant);
+    } else if (m.kind == 2) {
+      rc = launch_dict_jobs(base, (const DictJob*)m.d_jobs, m.njobs, m.grid);
+    } else {
+      // a pinned single-stream variant: host job (d_jobs is a host pointer)
+      const RleJob& J = *(const RleJob*)m.d_jobs;
+      unsigned long long* const saved = base->d_err;  // the job's own error record
+      if (J.err) base->d_err = J.err;
+      rc = launch_rlev2(base, J.src, J.src_len, (int)J.is_signed, J.segtab, J.nsegs, false, 0, 0, J.nvalues, J.dst, 8);
+      base->d_err = saved;
+    }
+  }
+  if (!joined) {  // join what was forked (also after a failure)
+    const int jr = join();
+    if (jr && !rc) rc = jr;
+  }
+  return rc;
+}
+
+int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
+  std::vector<MultiLaunch> ls;
+  const int rc = plan_rlev2_multi(ctx, jobs, njobs, ls);
+  return rc ? rc : run_multi(ctx, ls);
 }
 
 }  // namespace orcg
