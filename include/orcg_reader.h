@@ -250,8 +250,27 @@ typedef struct orcg_reader_metrics {
   uint64_t read_range_cache_hits;
   uint64_t read_range_cache_misses;
 } orcg_reader_metrics;
+/* Semantics (ReaderMetrics, c++/include/orc/Reader.hh:59-76; the reference
+ * fills them only when built with BUILD_CPP_ENABLE_METRICS):
+ *  - ReaderCall / ReaderInclusiveLatencyUs: per caller-facing call
+ *    (orcg_reader_read_stripe[s], orcg_row_reader_next), as the reference
+ *    times RowReaderImpl::next (Reader.cc:1393); a row reader's prefetch
+ *    decodes run inside them or ahead of them;
+ *  - DecompressionCall / DecompressionLatencyUs: chunks inflated and host time;
+ *  - DecodingCall / ByteDecodingCall: integer-RLE / byte-RLE streams decoded
+ *    (one stream decode = one call, the reference counts next() calls);
+ *  - DecodingLatencyUs / ByteDecodingLatencyUs: with metrics timing on
+ *    (orcg_reader_set_metrics_timing), device time of the integer-RLE and
+ *    byte-RLE launches from HIP events; off: DecodingLatencyUs is each
+ *    stripe's device decode phase and ByteDecodingLatencyUs stays 0;
+ *  - IOCount / IOBlockingLatencyUs: stream reads and their page-in time (the
+ *    file is mapped; the reference preads each stream);
+ *  - Selected/EvaluatedRowGroupCount: 0 (no search arguments), as the
+ *    reference without SargsApplier; ReadRangeCacheHits/Misses: 0 (no
+ *    read-range cache). */
 int orcg_reader_get_metrics(orcg_reader* r, orcg_reader_metrics* out);
 int orcg_reader_reset_metrics(orcg_reader* r);
+int orcg_reader_set_metrics_timing(orcg_reader* r, int on);
 /* RLEv2 streams of the last read decoded by a stripe's multi-stream launches
  * (every stream whose value count is known on the host: one launch per
  * kernel instance per stripe instead of one per stream). */

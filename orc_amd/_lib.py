@@ -167,6 +167,7 @@ SIGNATURES += [
     ("orcg_reader_last_stream_stats", [vp, ctypes.POINTER(u64)], i32),
     ("orcg_reader_get_metrics", [vp, ctypes.POINTER(u64)], i32),
     ("orcg_reader_reset_metrics", [vp], i32),
+    ("orcg_reader_set_metrics_timing", [vp, i32], i32),
     ("orcg_reader_content_length", [vp], u64),
     ("orcg_reader_software_version", [vp], cp),
     ("orcg_reader_num_metadata", [vp], u32),

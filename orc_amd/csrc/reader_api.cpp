@@ -109,42 +109,53 @@ bool is_supported(const file::TypeInfo& t, const std::string& writer_tz) {
   return k <= ORCG_TYPE_CHAR || k == ORCG_TYPE_DATE || k == ORCG_TYPE_VARCHAR;
 }
 
-// Caching device allocator: blocks are recycled stripe to stripe.
+// Device arena of a decoded stripe: allocations bump through one hipMalloc'd
+// chunk and are all released together when the slot decodes its next stripe,
+// so a stripe's buffers are contiguous (the row reader copies them to the
+// host in a few large D2H copies). A stripe that outgrows the chunk takes a
+// new one; the next stripe then starts from one chunk of the combined size.
 struct DevPool {
   int device = 0;
-  std::multimap<size_t, void*> free_blocks;
-  std::vector<std::pair<void*, size_t>> used;
+  std::vector<std::pair<uint8_t*, size_t>> chunks;  // the last is the active one
+  size_t off = 0;                                   // bump offset in the active chunk
+  size_t want = 0;                                  // bytes the last stripe used (all chunks)
+  size_t used_now = 0;
+  size_t hint = 0;                                  // the caller's estimate for a fresh slot
   ~DevPool() {
-    release_all();
-    for (auto& kv : free_blocks) (void)hipFree(kv.second);
+    for (auto& c : chunks) (void)hipFree(c.first);
   }
   void release_all() {
-    for (auto& u : used) free_blocks.emplace(u.second, u.first);
-    used.clear();
+    if (chunks.size() > 1 || (!chunks.empty() && chunks.back().second < want)) {
+      // consolidate: one chunk for the whole of the last stripe
+      for (auto& c : chunks) (void)hipFree(c.first);
+      chunks.clear();
+    }
+    want = std::max(want, used_now);
+    off = 0;
+    used_now = 0;
   }
   void* get(size_t bytes) {
     bytes = std::max<size_t>(256, (bytes + 255) & ~(size_t)255);
-    auto it = free_blocks.lower_bound(bytes);
-    if (it != free_blocks.end() && it->first <= 2 * bytes + (1 << 20)) {
-      void* p = it->second;
-      const size_t sz = it->first;
-      free_blocks.erase(it);
-      used.emplace_back(p, sz);
-      return p;
-    }
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
-      (void)hipGetLastError();  // the failure must not stick to a later launch check
-      // drop cached blocks and retry once
-      for (auto& kv : free_blocks) (void)hipFree(kv.second);
-      free_blocks.clear();
-      if (hipMalloc(&p, bytes) != hipSuccess) {
-        static const bool dbg = getenv("ORCG_DEBUG_ALLOC") != nullptr;
-        if (dbg) fprintf(stderr, "orcg: device allocation of %zu bytes failed\n", bytes);
-        return nullptr;
+    used_now += bytes;
+    if (chunks.empty() || off + bytes > chunks.back().second) {
+      const size_t cap = std::max<size_t>({bytes + (bytes >> 2), want + (want >> 3), hint, size_t(1) << 20});
+      uint8_t* p = nullptr;
+      if (hipMalloc((void**)&p, cap) != hipSuccess) {
+        (void)hipGetLastError();  // the failure must not stick to a later launch check
+        if (hipMalloc((void**)&p, bytes) != hipSuccess) {
+          (void)hipGetLastError();
+          static const bool dbg = getenv("ORCG_DEBUG_ALLOC") != nullptr;
+          if (dbg) fprintf(stderr, "orcg: device allocation of %zu bytes failed\n", bytes);
+          return nullptr;
+        }
+        chunks.push_back({p, bytes});
+      } else {
+        chunks.push_back({p, cap});
       }
+      off = 0;
     }
-    used.emplace_back(p, bytes);
+    void* p = chunks.back().first + off;
+    off += bytes;
     return p;
   }
 };
@@ -214,6 +225,9 @@ struct HostStage {
   uint64_t ngroups = 0;    // row groups with row-index positions (0: host plans only)
   uint64_t n_pos = 0, n_plan = 0;  // RLE streams cut by the row index / by a host plan
   uint64_t n_chunks = 0;            // compression chunks inflated (ReaderMetrics::DecompressionCall)
+  uint64_t n_io = 0;                // stream reads (ReaderMetrics::IOCount)
+  double t_io = 0;                  // their blocking time: page-ins of the mapped stripe (IOBlockingLatencyUs)
+  uint64_t io_sink = 0;
   uint64_t rows_off = 0;   // staging offset of int64 rows[g] = g * stride
   // room kept past the prepared bytes for the upload's tail (read-back block
   // and job arena, upload_tail_bytes): upload_and_decode never reallocates
@@ -271,6 +285,13 @@ struct DevSlot {
   std::vector<ColOut> out;
 };
 
+// A timed pair of events around a stripe's integer-RLE (kind 0) or byte-RLE
+// (kind 1) launches (ReaderMetrics with metrics timing)
+struct EvPair {
+  hipEvent_t a, b;
+  int kind;
+};
+
 struct orcg_reader {
   // serialises decodes: the reader's own reads and the row readers' prefetch
   // workers share its decode state (stages, batch tables, checks)
@@ -303,7 +324,7 @@ struct orcg_reader {
   PostScript ps;
   Footer footer;
   std::string last_error;
-  HostStage stages[2];
+  HostStage stages[3];  // read_stripes: stripe i in stages[i % 3]
   bool decimal_as_long = false;  // PostScript version 1.9999 (UNSTABLE-PRE-2.0): Decimal64V2 columns (Reader.cc:1693-1699)
   int32_t hive11_scale = 6;  // RowReaderOptions::forcedScaleOnHive11Decimal (Reader.cc RowReaderOptionsPrivate: 6)
   bool hive11_throw = true;  // RowReaderOptions::throwOnHive11DecimalOverflow (default true)
@@ -316,43 +337,109 @@ struct orcg_reader {
   double timings[5] = {0, 0, 0, 0, 0};
   uint64_t stream_stats[2] = {0, 0};  // last read: RLE streams cut by the row index, by host plans
   // ReaderMetrics (Reader.hh:59-76) over the reader's life, in orcg_reader_metrics
-  // order; updated under mu (every decode holds it)
-  uint64_t metrics[14] = {};
+  // order; atomics, as the reference's (the caller's thread counts next()
+  // calls while a row reader's worker decodes)
+  enum {
+    kMReaderCall, kMReaderLatency, kMDecompressCall, kMDecompressLatency, kMDecodeCall, kMDecodeLatency,
+    kMByteCall, kMByteLatency, kMIOCount, kMIOLatency, kMSelectedRG, kMEvaluatedRG, kMCacheHits, kMCacheMisses
+  };
+  std::atomic<uint64_t> metrics[14] = {};
+  void madd(int i, uint64_t v) { metrics[i].fetch_add(v, std::memory_order_relaxed); }
+  // DecodingLatencyUs / ByteDecodingLatencyUs from HIP events around the
+  // integer-RLE and byte-RLE launches of a stripe (orcg_reader_set_metrics_timing;
+  // off: DecodingLatencyUs is the stripe's device phase, ByteDecoding 0)
+  bool metrics_timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  hipEvent_t ev_get() {
+    if (ev_pool.empty()) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      return e;
+    }
+    hipEvent_t e = ev_pool.back();
+    ev_pool.pop_back();
+    return e;
+  }
+  // brackets the launches `f` enqueues on ctx->stream with a timed event pair
+  template <class Fn>
+  int timed(int kind, Fn&& f) {
+    if (!metrics_timing) return f();
+    hipEvent_t a = ev_get(), b = ev_get();
+    if (a) (void)hipEventRecord(a, ctx->stream);
+    const int rc = f();
+    if (b) (void)hipEventRecord(b, ctx->stream);
+    if (a && b) F->ev_used.push_back(EvPair{a, b, kind});
+    else {
+      if (a) ev_pool.push_back(a);
+      if (b) ev_pool.push_back(b);
+    }
+    return rc;
+  }
+  // after the stripe's synchronisation: the pairs' times into the metrics
+  void collect_event_times() {
+    double us[2] = {0, 0};
+    for (const EvPair& p : F->ev_used) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) us[p.kind] += ms * 1e3;
+      ev_pool.push_back(p.a);
+      ev_pool.push_back(p.b);
+    }
+    F->ev_used.clear();
+    madd(kMDecodeLatency, (uint64_t)us[0]);
+    madd(kMByteLatency, (uint64_t)us[1]);
+  }
   uint64_t batched_streams = 0;       // last read: RLEv2 streams decoded by multi-stream launches
   uint64_t stage_bytes = 0;           // last read: bytes uploaded (decompressed streams + plans)
 
-  // Checks whose operands are device scalars (dictionary blob size, varint
-  // counts, string bytes): their D2H copies are queued on the stream and the
-  // checks run, in column order, after the stripe's one synchronisation
-  // instead of a synchronisation each. The reference makes them inline.
-  uint64_t* h_defer = nullptr;
-  size_t defer_cap = 0, defer_used = 0;
-  // (column, check): run in column order with the columns' device errors
-  std::vector<std::pair<uint32_t, std::function<int()>>> checks;
+  // A stripe between its launches (issue) and its host checks (finish): its
+  // stage and slot, the checks whose operands are device scalars (dictionary
+  // blob size, varint counts, string bytes: their D2H copies are queued on
+  // the stream and the checks run, in column order, after the stripe's one
+  // synchronisation instead of a synchronisation each; the reference makes
+  // them inline), the pinned read-back mirror, the inline failure, and the
+  // event after the stripe's last copy. read_stripes keeps two in flight:
+  // stripe i + 1 is issued before stripe i is finished.
+  struct Flight {
+    HostStage* hs = nullptr;
+    DevSlot* ds = nullptr;
+    uint64_t* h_defer = nullptr;
+    size_t defer_cap = 0, defer_used = 0;
+    // (column, check): run in column order with the columns' device errors
+    std::vector<std::pair<uint32_t, std::function<int()>>> checks;
+    // the read-back block's pinned mirror (valid after the stripe's copy)
+    uint64_t* h_rb = nullptr;
+    size_t h_rb_cap = 0, rb_words = 0, rb_used = 0;
+    std::vector<EvPair> ev_used;  // metrics timing events
+    hipEvent_t done = nullptr;    // recorded after the read-back copy
+    bool enqueued = false;        // done / the read-back copy belong to this issue
+    int rc = ORCG_OK;             // the inline (host-detected) failure of the issue
+    uint32_t err_col = 0;
+    std::string err_msg;
+    double t0 = 0, t1 = 0;
+  };
+  Flight flights[2];
+  Flight* F = &flights[0];
   // the column decode() is working on, and the column of the first inline
   // (host-detected) failure of this stripe
   static constexpr uint32_t kNoCol = 0xffffffffu;
   uint32_t cur_col = kNoCol, err_col = kNoCol;
   int first_error(int inline_rc);
-  // the read-back block's pinned mirror (valid after first_error's copy)
-  uint64_t* h_rb = nullptr;
-  size_t h_rb_cap = 0, rb_words = 0, rb_slot0 = 0, rb_used = 0;
   // `count` words of the read-back block: the device address a kernel writes,
   // and (*host) where the host reads it after the stripe's synchronisation
   uint64_t* rb_alloc(size_t count, const uint64_t** host) {
-    if (!D->d_rb || rb_used + count > rb_words) return nullptr;
-    uint64_t* d = D->d_rb + rb_used;
-    *host = h_rb + rb_used;
-    rb_used += count;
+    if (!D->d_rb || F->rb_used + count > F->rb_words) return nullptr;
+    uint64_t* d = D->d_rb + F->rb_used;
+    *host = F->h_rb + F->rb_used;
+    F->rb_used += count;
     return d;
   }
   const uint64_t* defer(const void* d_src, size_t count) {
     // a value in the read-back block rides its one copy
-    if (D && D->d_rb && (const uint64_t*)d_src >= D->d_rb && (const uint64_t*)d_src + count <= D->d_rb + rb_words)
-      return h_rb + ((const uint64_t*)d_src - D->d_rb);
-    if (defer_used + count > defer_cap) return nullptr;
-    uint64_t* h = h_defer + defer_used;
-    defer_used += count;
+    if (D && D->d_rb && (const uint64_t*)d_src >= D->d_rb && (const uint64_t*)d_src + count <= D->d_rb + F->rb_words)
+      return F->h_rb + ((const uint64_t*)d_src - D->d_rb);
+    if (F->defer_used + count > F->defer_cap) return nullptr;
+    uint64_t* h = F->h_defer + F->defer_used;
+    F->defer_used += count;
     if (hipMemcpyAsync(h, d_src, count * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) return nullptr;
     return h;
   }
@@ -385,9 +472,14 @@ struct orcg_reader {
   ~orcg_reader() {
     slots.clear();
     if (mapped) munmap(mapped, file_len);
-    if (h_defer) (void)hipHostFree(h_defer);
     if (h_sync) (void)hipHostFree(h_sync);
-    if (h_rb) (void)hipHostFree(h_rb);
+    for (Flight& f : flights) {
+      if (f.h_defer) (void)hipHostFree(f.h_defer);
+      if (f.h_rb) (void)hipHostFree(f.h_rb);
+      for (const EvPair& p : f.ev_used) ev_pool.push_back(p.a), ev_pool.push_back(p.b);
+      if (f.done) (void)hipEventDestroy(f.done);
+    }
+    for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
   }
   int fail(int status, const std::string& m) {
     if (err_col == kNoCol) err_col = cur_col;
@@ -396,7 +488,7 @@ struct orcg_reader {
     return status;
   }
   int fail_ctx(int rc) { return fail(rc, ctx ? ctx->last_error : std::string("device error")); }
-  // a failure outside a decode (argument checks of the caller's thread):
+  // a failure outside a decode (argument F->checks of the caller's thread):
   // last_error is shared with the row readers' workers, so under mu
   int fail_user(int status, const std::string& m) {
     std::lock_guard<std::mutex> lk(mu);
@@ -411,9 +503,14 @@ struct orcg_reader {
   }
 
   int open_tail();
-  int prepare(uint64_t s, HostStage& hs) const;
+  // (sel: the column selection of the read it prepares for; prepare reads
+  // nothing else the decodes change, so it runs without mu)
+  int prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& sel) const;
+  int prepare(uint64_t s, HostStage& hs) const { return prepare(s, hs, selected); }
   int read_stripes(uint64_t first, uint64_t count);
-  int upload_and_decode(HostStage& hs, DevSlot& ds);
+  int upload_and_decode(HostStage& hs, DevSlot& ds);  // issue + finish
+  void issue(HostStage& hs, DevSlot& ds, Flight& fl);
+  int finish(Flight& fl);
   // d_in_count (may be null): in_count is on the device (the parent's
   // non-null rows), in_count is then an upper bound; in_col: the column whose
   // mask in_nn is
@@ -422,7 +519,7 @@ struct orcg_reader {
   // Columns whose value streams take a device-resident value count (RLEv2
   // through the tiled instances): their PRESENT decode's non-null count is
   // not read back mid-stripe (one stream synchronisation per nullable column
-  // saved); has_nulls is settled with the stripe's checks.
+  // saved); has_nulls is settled with the stripe's F->checks.
   bool device_counts(const Col& c) const;
   // Whether decode(id) launches device work: false when everything it needs
   // came from the stripe's batched launches (streams, dictionaries)
@@ -660,12 +757,12 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   int rc = segments(c, slot, false, &d_seg, &nseg);
   if (rc) return rc;
   const int sg = is_signed ? 1 : 0;
-  ++metrics[4];  // DecodingCall
-  if (v1)
-    rc = launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
-  else
-    rc = dcount ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, dcount)
-                : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
+  madd(kMDecodeCall, 1);
+  rc = timed(0, [&]() -> int {
+    if (v1) return launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
+    return dcount ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, dcount)
+                  : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
+  });
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
 
@@ -710,7 +807,7 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
       d.is_signed = is_signed ? 1u : 0u;
       v1_segs.push_back(d);
     }
-    ++metrics[4];  // DecodingCall
+    madd(kMDecodeCall, 1);
     batched[(uint64_t)id * 8 + (uint64_t)slot] = {out, count};
     return ORCG_OK;
   }
@@ -738,14 +835,14 @@ int orcg_reader::queue_stream(uint32_t id, int slot, bool is_signed, uint64_t co
   j.is_signed = is_signed ? 1u : 0u;
   j.err = D->d_errs + id;
   batch.push_back(j);
-  ++metrics[4];  // DecodingCall
+  madd(kMDecodeCall, 1);
   batched[(uint64_t)id * 8 + (uint64_t)slot] = {out, count};
   return ORCG_OK;
 }
 
 // A dictionary column whose streams are both batched: its offsets and row
 // gather join the stripe's dictionary launch (decode() then only wires the
-// outputs and registers its checks).
+// outputs and registers its F->checks).
 int orcg_reader::queue_dict(uint32_t id, uint64_t n) {
   Col& c = H->cols[id];
   const uint64_t D_ = c.dict_size;
@@ -827,8 +924,10 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   uint64_t nseg;
   int rc = segments(c, slot, boolean, &d_seg, &nseg);
   if (rc) return rc;
-  ++metrics[6];  // ByteDecodingCall
-  rc = launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count);
+  madd(kMByteCall, 1);
+  rc = timed(1, [&]() -> int {
+    return launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count);
+  });
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
 
@@ -892,14 +991,14 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   c.has_nulls = nn != nullptr && (d_nonnull != nullptr || nonnull < n);
   if (in_nn && !c.s[kSlotPresent].present) c.has_nulls = true;  // incoming mask copied (:97-101)
   c.nn = c.has_nulls ? nn : nullptr;
-  // provisional has_nulls: settled by the stripe's checks (column order:
+  // provisional has_nulls: settled by the stripe's F->checks (column order:
   // a parent's before its children's)
   if (c.s[kSlotPresent].present && d_nonnull) {
     const uint64_t* h = defer(d_nonnull, 1);
     if (!h) return fail(ORCG_DEVICE_ERROR, "D2H of the non-null count failed");
     c.nulls_deferred = true;
     Col* cp = &c;
-    checks.emplace_back(cur_col, [cp, h, n]() -> int {
+    F->checks.emplace_back(cur_col, [cp, h, n]() -> int {
       if (*h >= n) {
         cp->has_nulls = false;
         cp->nn = nullptr;
@@ -909,7 +1008,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
   } else if (in_nn && !c.s[kSlotPresent].present && in_col && in_col->nulls_deferred) {
     c.nulls_deferred = true;
     Col* cp = &c;
-    checks.emplace_back(cur_col, [cp, in_col]() -> int {
+    F->checks.emplace_back(cur_col, [cp, in_col]() -> int {
       if (!in_col->has_nulls) {  // the parent had no nulls after all: no mask was passed down
         cp->has_nulls = false;
         cp->nn = nullptr;
@@ -958,7 +1057,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if ((rc = launch_exclusive_scan(ctx, counts, ntiles, base))) return fail_ctx(rc);
       const uint64_t* total = defer(base + ntiles, 1);
       if (!total) return fail(ORCG_DEVICE_ERROR, "D2H of the varint count failed");
-      checks.emplace_back(cur_col, [this, total, nonnull, cid]() -> int {
+      F->checks.emplace_back(cur_col, [this, total, nonnull, cid]() -> int {
         return *total < nonnull ? fail(ORCG_PARSE_ERROR, "Read past end of stream in Decimal64ColumnReader column " +
                                                              cid + " kind DATA")
                                 : ORCG_OK;
@@ -998,7 +1097,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
         const uint64_t* kept = defer(kept_d, 1);
         if (!kept) return fail(ORCG_DEVICE_ERROR, "D2H of the kept decimal count failed");
         Col* cp = &c;
-        checks.emplace_back(cur_col, [cp, kept, rnn, n]() -> int {
+        F->checks.emplace_back(cur_col, [cp, kept, rnn, n]() -> int {
           if (*kept < n) {
             cp->has_nulls = true;
             cp->nn = rnn;
@@ -1061,14 +1160,14 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     const auto dd = dict ? dict_done.find(id) : dict_done.end();
     if (dd != dict_done.end()) {
       // batched (queue_dict): offsets, summary and gather come from the
-      // stripe's dictionary launch; the reference's checks, in its order
+      // stripe's dictionary launch; the reference's F->checks, in its order
       const std::string cid = std::to_string(id);
       const uint64_t* h = dd->second.h_summary;
       StreamBuf& db = c.s[kSlotDict];
       Col* cp = &c;
       const bool db_present = db.present;
       const uint64_t db_len = db.present ? db.len : 0;
-      checks.emplace_back(cur_col, [this, h, cp, db_present, db_len, cid]() -> int {
+      F->checks.emplace_back(cur_col, [this, h, cp, db_present, db_len, cid]() -> int {
         if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
         if (h[0] > 0 && !db_present)
           return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
@@ -1110,7 +1209,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       Col* cp = &c;
       const bool db_present = db.present;
       const uint64_t db_len = db.present ? db.len : 0;
-      checks.emplace_back(cur_col, [this, h, cp, db_present, db_len, cid]() -> int {
+      F->checks.emplace_back(cur_col, [this, h, cp, db_present, db_len, cid]() -> int {
         if (h[1]) return fail(ORCG_PARSE_ERROR, "Negative dictionary entry length for column " + cid);
         if (h[0] > 0 && !db_present)
           return fail(ORCG_PARSE_ERROR, "DICTIONARY_DATA stream not found in StringDictionaryColumn for column " + cid);
@@ -1151,7 +1250,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       const uint64_t* need = defer(dstart + nonnull, 1);
       if (!need) return fail(ORCG_DEVICE_ERROR, "D2H of the string bytes failed");
       const uint64_t blob_len = c.blob_len;
-      checks.emplace_back(cur_col, [this, need, blob_len]() -> int {
+      F->checks.emplace_back(cur_col, [this, need, blob_len]() -> int {
         return *need > blob_len ? fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next") : ORCG_OK;
       });
       if (row_nn) {
@@ -1404,7 +1503,7 @@ static bool long_runs(const uint8_t* p, uint64_t len) {
   return runs > 0 && pos >= 96 * runs;
 }
 
-int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
+int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& selected) const {
   hs.stripe = s;
   hs.rc = ORCG_OK;
   hs.err.clear();
@@ -1465,6 +1564,22 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
     Need nd{st.column, slot, {}, st.offset};
     if (!split_chunks(file, st.offset, st.length, ps.compression, nd.chunks, err)) return hs.fail(ORCG_PARSE_ERROR, err);
     needs.push_back(std::move(nd));
+  }
+  // I/O (ReaderMetrics::IOCount / IOBlockingLatencyUs): the reference preads
+  // each stream (SeekableFileInputStream); this reader maps the file, so its
+  // blocking I/O is the page-in of the streams' byte ranges: one touch per
+  // page, timed (page-cache hits cost ~nothing, cold pages their read)
+  {
+    const double ti = now_s();
+    uint64_t sink = 0;
+    for (const Need& nd : needs)
+      for (const Chunk& ch : nd.chunks) {
+        const uint8_t* b = file + ch.src_off;
+        for (uint64_t o = 0; o < ch.src_len; o += 4096) sink += ((const volatile uint8_t*)b)[o];
+      }
+    hs.io_sink = sink;
+    hs.t_io = now_s() - ti;
+    hs.n_io = needs.size() + 1;  // + the stripe footer
   }
   // staging: every chunk gets a slot of its maximum size, compacted after
   uint64_t at = 0;
@@ -1757,30 +1872,28 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs) const {
 // The stripe's first error, in column order (type ids are pre-order, the
 // order decode() visits the columns): for each column up to the one that
 // failed inline (`inline_rc`, detected on the host while launching), its
-// deferred checks, then its device error record (the first bad value of its
+// deferred F->checks, then its device error record (the first bad value of its
 // kernels), as the reference raises them while reading that column; then the
 // inline failure itself; then the context's own record.
 int orcg_reader::first_error(int inline_rc) {
   const std::string inline_msg = last_error;
   const uint32_t inline_col = err_col;
   cur_col = kNoCol;
-  // one copy brings back the error records, the non-null counts and the
-  // summary slots (rb_alloc), then one synchronisation
+  // the stripe's read-back copy (error records, non-null counts, summary
+  // slots) and its deferred copies were queued by issue(): wait for them
   const size_t nc = H->cols.size();
-  if (hipMemcpyAsync(h_rb, D->d_rb, 8 * rb_used, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess)
-    return fail(ORCG_DEVICE_ERROR, "read error records");
-  if (hipStreamSynchronize(ctx->stream) != hipSuccess) return fail(ORCG_DEVICE_ERROR, "stream synchronize failed");
-  std::vector<unsigned long long> rec(h_rb, h_rb + nc);
+  if (hipEventSynchronize(F->done) != hipSuccess) return fail(ORCG_DEVICE_ERROR, "stream synchronize failed");
+  std::vector<unsigned long long> rec(F->h_rb, F->h_rb + nc);
   const uint32_t last = inline_rc ? (inline_col == kNoCol ? 0u : inline_col) : (uint32_t)nc;
   // checks grouped by column once (stable: a column's checks keep their
   // order), then one walk over columns and checks together
-  std::stable_sort(checks.begin(), checks.end(),
+  std::stable_sort(F->checks.begin(), F->checks.end(),
                    [](const std::pair<uint32_t, std::function<int()>>& a,
                       const std::pair<uint32_t, std::function<int()>>& b) { return a.first < b.first; });
   size_t ci = 0;
   for (uint32_t col = 0; col < nc && col <= last; ++col) {
-    for (; ci < checks.size() && checks[ci].first <= col; ++ci) {
-      const int rc = checks[ci].second();
+    for (; ci < F->checks.size() && F->checks[ci].first <= col; ++ci) {
+      const int rc = F->checks[ci].second();
       if (rc) return rc;
     }
     if (rec[col] != kNoError) {
@@ -1796,13 +1909,13 @@ int orcg_reader::first_error(int inline_rc) {
     }
   }
   if (inline_rc) return fail(inline_rc, inline_msg);
-  for (auto& ch : checks)
+  for (auto& ch : F->checks)
     if (ch.first >= nc) {
       const int rc = ch.second();
       if (rc) return rc;
     }
   // the context's own record (launches outside a column's scope)
-  const unsigned long long own = h_rb[2 * nc];
+  const unsigned long long own = F->h_rb[2 * nc];
   if (own != kNoError) {
     const uint32_t code = (uint32_t)(own & 0xff);
     ctx->last_error_value = own >> 8;
@@ -1811,9 +1924,17 @@ int orcg_reader::first_error(int inline_rc) {
   return ORCG_OK;
 }
 
-// Device half: one H2D of the staging buffer, then every selected column.
-int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
-  const double t0 = now_s();
+// Device half, launch side: one H2D of the staging buffer (streams, the
+// initialised read-back block, the batched launches' job tables), the
+// batched launches, every selected column's launches, the read-back copy and
+// the flight's event. Host checks wait for finish().
+void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
+  F = &fl;
+  fl.hs = &hs;
+  fl.ds = &ds;
+  fl.t0 = now_s();
+  fl.rc = ORCG_OK;
+  fl.enqueued = false;
   // Launch checks read hipGetLastError (per host thread): drop a failure a
   // call whose result was already checked or deliberately ignored (frees in
   // destructors, a retried allocation) left behind, so it cannot surface as
@@ -1823,8 +1944,24 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
     static const bool dbg = getenv("ORCG_DEBUG_STALE") != nullptr;
     if (dbg && stale != hipSuccess) fprintf(stderr, "orcg: stale HIP error before upload: %s\n", hipGetErrorString(stale));
   }
+  cur_col = err_col = kNoCol;
+  auto early = [&](int rc) {  // a failure before anything was enqueued
+    fl.rc = rc;
+    fl.err_col = err_col;
+    fl.err_msg = last_error;
+    fl.t1 = now_s();
+    H = nullptr;
+    D = nullptr;
+  };
   ds.stripe = hs.stripe;
   ds.pool.release_all();
+  // a fresh slot's first chunk: the staging plus ~16 bytes per row and
+  // selected column (outputs and scratch); later stripes use what it took
+  {
+    size_t nsel = 0;
+    for (size_t i = 0; i < hs.cols.size(); ++i) nsel += selected[i] && hs.cols[i].supported ? 1 : 0;
+    ds.pool.hint = hs.used + hs.slack + 16 * nsel * footer.stripes[hs.stripe].num_rows + (1u << 20);
+  }
   const size_t nc = hs.cols.size();
   const uint64_t nrows_stripe = footer.stripes[hs.stripe].num_rows;
   // after the streams: the read-back block (error records 0xff.., non-null
@@ -1832,30 +1969,43 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   // tables): one upload carries the stripe, its initialised counters and
   // its job tables
   const uint64_t rb_off = (hs.used + 255) & ~(uint64_t)255;
-  rb_words = rb_words_for(nc);
-  rb_slot0 = rb_used = 2 * nc + 1;  // word 2 nc: the context's own record during this stripe
-  const uint64_t arena_off = (rb_off + 8 * rb_words + 255) & ~(uint64_t)255;
+  fl.rb_words = rb_words_for(nc);
+  fl.rb_used = 2 * nc + 1;  // word 2 nc: the context's own record during this stripe
+  const uint64_t arena_off = (rb_off + 8 * fl.rb_words + 255) & ~(uint64_t)255;
   const uint64_t arena_cap = arena_bytes_for(nc, v1_segments(hs), (nrows_stripe + 2047) / 2048 + 1);
   const uint64_t total = arena_off + arena_cap;
-  if (!hs.ensure(total + 64, hs.used)) return fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed");
+  if (!hs.ensure(total + 64, hs.used)) return early(fail(ORCG_OUT_OF_MEMORY, "pinned staging allocation failed"));
   memset(hs.h + rb_off, 0xff, 8 * nc);
-  memset(hs.h + rb_off + 8 * nc, 0, 8 * (rb_words - nc));
+  memset(hs.h + rb_off + 8 * nc, 0, 8 * (fl.rb_words - nc));
   memset(hs.h + rb_off + 8 * (2 * nc), 0xff, 8);
-  debug_stale("upload: staging ensured");
   ds.d_stage = (uint8_t*)ds.pool.get(total + 64);
-  if (!ds.d_stage) return fail_oom(__LINE__);
-  debug_stale("upload: device slot");
+  if (!ds.d_stage) return early(fail_oom(__LINE__));
   ds.d_rb = (uint64_t*)(ds.d_stage + rb_off);
   ds.d_errs = (unsigned long long*)ds.d_rb;
   ds.d_ones = ds.d_rb + nc;
-  if (h_rb_cap < rb_words) {
-    if (h_rb) (void)hipHostFree(h_rb);
-    h_rb = nullptr;
-    h_rb_cap = 0;
-    if (hipHostMalloc((void**)&h_rb, rb_words * 8, hipHostMallocDefault) != hipSuccess)
-      return fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed");
-    h_rb_cap = rb_words;
+  if (fl.h_rb_cap < fl.rb_words) {
+    if (fl.h_rb) (void)hipHostFree(fl.h_rb);
+    fl.h_rb = nullptr;
+    fl.h_rb_cap = 0;
+    if (hipHostMalloc((void**)&fl.h_rb, fl.rb_words * 8, hipHostMallocDefault) != hipSuccess)
+      return early(fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed"));
+    fl.h_rb_cap = fl.rb_words;
   }
+  if (!fl.done && hipEventCreateWithFlags(&fl.done, hipEventDisableTiming) != hipSuccess) {
+    fl.done = nullptr;
+    return early(fail(ORCG_DEVICE_ERROR, "event creation failed"));
+  }
+  const size_t need_defer = 4 * nc + 16;
+  if (fl.defer_cap < need_defer) {
+    if (fl.h_defer) (void)hipHostFree(fl.h_defer);
+    fl.h_defer = nullptr;
+    fl.defer_cap = 0;
+    if (hipHostMalloc((void**)&fl.h_defer, need_defer * 8, hipHostMallocDefault) != hipSuccess)
+      return early(fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed"));
+    fl.defer_cap = need_defer;
+  }
+  fl.defer_used = 0;
+  fl.checks.clear();
   H = &hs;
   D = &ds;
   // the context's own record for this stripe rides the read-back block (the
@@ -1866,25 +2016,13 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
     ~OwnRecord() { c->d_err = saved; }
   } own_rec{ctx, ctx->d_err};
   ctx->d_err = (unsigned long long*)(ds.d_rb + 2 * nc);
-  const size_t need_defer = 4 * nc + 16;
-  if (defer_cap < need_defer) {
-    if (h_defer) (void)hipHostFree(h_defer);
-    h_defer = nullptr;
-    defer_cap = 0;
-    if (hipHostMalloc((void**)&h_defer, need_defer * 8, hipHostMallocDefault) != hipSuccess)
-      return fail(ORCG_OUT_OF_MEMORY, "pinned allocation failed");
-    defer_cap = need_defer;
-  }
-  defer_used = 0;
-  checks.clear();
-  cur_col = err_col = kNoCol;
   batch.clear();
   v1_segs.clear();
   batched.clear();
   dict_batch.clear();
   dict_done.clear();
   launches.clear();
-  const uint64_t nrows = footer.stripes[hs.stripe].num_rows;
+  const uint64_t nrows = nrows_stripe;
   const int64_t* rg_rows = hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr;
   // the batch: streams (and dictionaries) whose counts the host knows, their
   // job tables staged into the arena before the upload
@@ -1905,27 +2043,56 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
     ctx->arena_h = ctx->arena_d = nullptr;
     ctx->arena_cap = 0;
   }
-  debug_stale("upload: batch planned");
   const uint64_t up = arena_off + ctx->arena_used;
   stage_bytes += up;
-  // (uploaded even after a failure above: first_error reads the records back)
+  // (uploaded even after a failure above: finish() reads the records back)
   const int urc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, up, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
   if (urc && !rc) rc = fail_ctx(urc);
-  // The decode's launches follow the copy on the same stream (side lanes
-  // wait on a fork event recorded after it): the synchronisation only splits
-  // the H2D phase out of the timings, so small stripes (configs[0]: ~50 KB of
-  // staging) skip it and count their copy in the decode phase.
-  if (!rc && hs.used >= (1u << 20) && (rc = sync_ctx(ctx))) rc = fail_ctx(rc);
-  const double t1 = now_s();
-  debug_stale("upload: copied");
-  if (!rc && !launches.empty() && (rc = run_multi(ctx, launches))) rc = fail_ctx(rc);
+  fl.t1 = now_s();
+  if (!rc && !launches.empty() && (rc = timed(0, [&]() -> int { return run_multi(ctx, launches); })))
+    rc = fail_ctx(rc);
   if (!rc) rc = decode(0, nrows, nullptr, nrows, rg_rows);
   batched_streams += batched.size();
-  (void)arena_off;
-  // queued copies land before the buffer is reused; then the first error in
-  // column order, as the reference raises them one column at a time
+  fl.rc = rc;
+  fl.err_col = err_col;
+  fl.err_msg = last_error;
+  // the read-back copy, then the flight's event (queued copies land before
+  // the buffers are reused)
+  if (hipMemcpyAsync(fl.h_rb, ds.d_rb, 8 * fl.rb_used, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipEventRecord(fl.done, ctx->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(ctx->stream);
+    if (!fl.rc) {
+      fl.rc = ORCG_DEVICE_ERROR;
+      fl.err_msg = "read error records";
+    }
+    // (the records are unreadable: finish() reports fl.rc)
+    memset(fl.h_rb, 0xff, 8 * fl.rb_used);
+    (void)hipEventRecord(fl.done, ctx->stream);
+  }
+  fl.enqueued = true;
+  H = nullptr;
+  D = nullptr;
+}
+
+// Device half, host side: the first error in column order, as the reference
+// raises them one column at a time, then the stripe's column views.
+int orcg_reader::finish(Flight& fl) {
+  F = &fl;
+  H = fl.hs;
+  D = fl.ds;
+  HostStage& hs = *fl.hs;
+  DevSlot& ds = *fl.ds;
+  int rc = fl.rc;
+  if (!fl.enqueued) {  // failed before anything was enqueued
+    H = nullptr;
+    D = nullptr;
+    return fail(rc, fl.err_msg);
+  }
+  err_col = fl.err_col;
+  last_error = fl.err_msg;
   rc = first_error(rc);
-  checks.clear();
+  fl.checks.clear();
   ds.out.assign(hs.cols.size(), ColOut());
   for (size_t i = 0; i < hs.cols.size(); ++i) {
     const Col& c = hs.cols[i];
@@ -1950,29 +2117,33 @@ int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
   H = nullptr;
   D = nullptr;
   const double t_end = now_s();
-  timings[3] += t1 - t0;
-  timings[4] += t_end - t1;
-  // ReaderMetrics: one stripe read = one reader call and one I/O (the stripe's
-  // byte range of the mapped file); the host phases come from prepare()
-  const uint64_t stride = footer.row_index_stride;
-  const uint64_t srows = footer.stripes[hs.stripe].num_rows;
-  metrics[0] += 1;
-  metrics[1] += (uint64_t)((hs.t_parse + hs.t_decomp + hs.t_plan + (t_end - t0)) * 1e6);
-  metrics[2] += hs.n_chunks;
-  metrics[3] += (uint64_t)(hs.t_decomp * 1e6);
-  metrics[5] += (uint64_t)((t_end - t1) * 1e6);
-  metrics[8] += 1;
-  metrics[9] += (uint64_t)(hs.t_parse * 1e6);
-  metrics[10] += stride ? (srows + stride - 1) / stride : (srows ? 1 : 0);
+  timings[3] += fl.t1 - fl.t0;
+  timings[4] += t_end - fl.t1;
+  // ReaderMetrics (ReaderCall / ReaderInclusiveLatencyUs are counted per
+  // caller-facing call: orcg_reader_read_stripe(s), orcg_row_reader_next):
+  // the stripe's decompression, I/O and decode work
+  madd(kMDecompressCall, hs.n_chunks);
+  madd(kMDecompressLatency, (uint64_t)(hs.t_decomp * 1e6));
+  madd(kMIOCount, hs.n_io);
+  madd(kMIOLatency, (uint64_t)(hs.t_io * 1e6));
+  if (metrics_timing) collect_event_times();
+  else madd(kMDecodeLatency, (uint64_t)((t_end - fl.t1) * 1e6));
   return rc;
 }
 
-// Stripes [first, first + count): one host thread prepares stripe i + 1
-// (decompression, plans) while the caller's thread uploads and decodes stripe
-// i; the two stages alternate (stripe i in stages[i & 1]), so the preparer
-// waits only for the decode of stripe i - 1 to release its stage. One thread
-// for the whole read: a thread per stripe cost more than a configs[0] stripe
-// decodes in.
+int orcg_reader::upload_and_decode(HostStage& hs, DevSlot& ds) {
+  issue(hs, ds, flights[0]);
+  return finish(flights[0]);
+}
+
+// Stripes [first, first + count), pipelined three ways: a host thread
+// prepares stripe i + 1 (decompression, plans) while the caller's thread
+// issues stripe i (upload, launches) and then finishes stripe i - 1 (its
+// synchronisation and host checks) -- so the GPU starts stripe i while the
+// host checks stripe i - 1. Stripe i lives in stages[i % 3] and
+// flights[i & 1]; the preparer of stripe i waits for stripe i - 3 to be
+// finished. One thread for the whole read: a thread per stripe cost more
+// than a configs[0] stripe decodes in.
 int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   if (!ctx) return fail(ORCG_INVALID_ARGUMENT, "reader has no device context");
   if (first > footer.stripes.size() || count > footer.stripes.size() - first)
@@ -1987,47 +2158,74 @@ int orcg_reader::read_stripes(uint64_t first, uint64_t count) {
   if (count == 0) return ORCG_OK;
   std::mutex pm;
   std::condition_variable pcv;
-  uint64_t prepared = 0, released = 0;  // stripes prepared; stripes whose stage the decode is done with
+  uint64_t prepared = 0, released = 0;  // stripes prepared; stripes finished (their stages free)
   bool quit = false;
   std::thread prep([&] {
     for (uint64_t k = 0; k < count; ++k) {
       {
         std::unique_lock<std::mutex> lk(pm);
-        pcv.wait(lk, [&] { return quit || k < released + 2; });  // stripe k - 2 released stages[k & 1]
+        pcv.wait(lk, [&] { return quit || k < released + 3; });  // stripe k - 3 released stages[k % 3]
         if (quit) return;
       }
-      prepare(first + k, stages[k & 1]);
+      prepare(first + k, stages[k % 3]);
       {
         std::lock_guard<std::mutex> lk(pm);
         prepared = k + 1;
       }
       pcv.notify_all();
-      if (stages[k & 1].rc) return;  // the decode raises it when it reaches stripe k
+      if (stages[k % 3].rc) return;  // the decode raises it when it reaches stripe k
     }
   });
-  int rc = ORCG_OK;
-  for (uint64_t k = 0; k < count && !rc; ++k) {
-    {
-      std::unique_lock<std::mutex> lk(pm);
-      pcv.wait(lk, [&] { return prepared > k; });
-    }
-    HostStage& cur = stages[k & 1];
-    timings[0] += cur.t_parse;
-    timings[1] += cur.t_decomp;
-    timings[2] += cur.t_plan;
-    stream_stats[0] += cur.n_pos;
-    stream_stats[1] += cur.n_plan;
-    if (cur.rc) {
-      rc = fail(cur.rc, cur.err);
-      break;
-    }
-    rc = upload_and_decode(cur, *slots[k]);
-    if (!rc) nslots = k + 1;
+  auto release = [&](uint64_t n) {
     {
       std::lock_guard<std::mutex> lk(pm);
-      released = k + 1;
+      released = n;
     }
     pcv.notify_all();
+  };
+  int rc = ORCG_OK;
+  bool pending = false;  // stripe k - 1 issued, not finished
+  for (uint64_t k = 0; k <= count; ++k) {
+    bool issued = false;
+    if (k < count) {
+      {
+        std::unique_lock<std::mutex> lk(pm);
+        pcv.wait(lk, [&] { return prepared > k; });
+      }
+      HostStage& cur = stages[k % 3];
+      timings[0] += cur.t_parse;
+      timings[1] += cur.t_decomp;
+      timings[2] += cur.t_plan;
+      stream_stats[0] += cur.n_pos;
+      stream_stats[1] += cur.n_plan;
+      if (cur.rc) {
+        if (pending) {
+          const int prc = finish(flights[(k - 1) & 1]);
+          if (!prc) nslots = k;
+          rc = prc ? prc : fail(cur.rc, cur.err);
+        } else {
+          rc = fail(cur.rc, cur.err);
+        }
+        pending = false;
+        break;
+      }
+      issue(cur, *slots[k], flights[k & 1]);
+      issued = true;
+    }
+    if (pending) {
+      const int prc = finish(flights[(k - 1) & 1]);
+      release(k);
+      if (prc) {
+        rc = prc;
+        if (issued) {  // let the issued stripe drain before its buffers go
+          (void)hipEventSynchronize(flights[k & 1].done);
+          issued = false;
+        }
+        break;
+      }
+      nslots = k;
+    }
+    pending = issued;
   }
   {
     std::lock_guard<std::mutex> lk(pm);
@@ -2177,20 +2375,51 @@ struct orcg_row_reader {
   // (every decode runs under r->mu with this row reader's options and
   // context as the reader's active ones, orcg_reader::Active; the reader's
   // own options are never touched)
-  // D2H of every decoded column of `dev` into the slab (one synchronisation)
+  // D2H of every decoded column of `dev` into the slab: the stripe's
+  // buffers sit in one device arena (DevPool), so sorted by address they
+  // merge into a few ranges (gaps up to 1 MB copied along), one copy each;
+  // then one synchronisation
   int copy_out(HostSlab& sl) {
     sl.out = dev->out;
-    // (column, field, bytes) of every decoded buffer
-    std::vector<std::pair<size_t, std::pair<int, uint64_t>>> bufs;
+    struct Buf {
+      size_t col;
+      int f;
+      const uint8_t* d;
+      uint64_t bytes;
+      size_t range;
+    };
+    std::vector<Buf> bufs;
     std::vector<std::pair<int, uint64_t>> cb;
     for (size_t i = 0; i < sl.out.size(); ++i) {
       if (!sl.out[i].decoded) continue;
       cb.clear();
       col_buffers(sl.out[i], r->footer.types[i], cb);
-      for (auto& x : cb) bufs.push_back({i, x});
+      for (auto& x : cb) bufs.push_back(Buf{i, x.first, (const uint8_t*)col_get(sl.out[i], x.first), x.second, 0});
+    }
+    std::vector<size_t> order(bufs.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return bufs[a].d < bufs[b].d; });
+    struct Range {
+      const uint8_t* d;
+      uint64_t bytes, hoff;
+    };
+    std::vector<Range> rs;
+    constexpr uint64_t kGap = 1u << 20;
+    for (size_t q : order) {
+      Buf& bf = bufs[q];
+      if (!rs.empty() && bf.d >= rs.back().d && bf.d <= rs.back().d + rs.back().bytes + kGap) {
+        const uint64_t end = (uint64_t)(bf.d - rs.back().d) + bf.bytes;
+        rs.back().bytes = std::max(rs.back().bytes, end);
+      } else {
+        rs.push_back(Range{bf.d, bf.bytes, 0});
+      }
+      bf.range = rs.size() - 1;
     }
     uint64_t total = 0;
-    for (auto& bb : bufs) total += (bb.second.second + 255) & ~(uint64_t)255;
+    for (Range& rg : rs) {
+      rg.hoff = total;
+      total += (rg.bytes + 255) & ~(uint64_t)255;
+    }
     if (total > sl.cap) {
       const double ta = now_s();
       pinned_free(sl.h);
@@ -2201,18 +2430,16 @@ struct orcg_row_reader {
       sl.cap = ncap;
       addp(3, now_s() - ta);
     }
-    uint64_t w = 0;
-    for (auto& bb : bufs) {
-      ColOut& o = sl.out[bb.first];
-      const int f = bb.second.first;
-      const uint64_t bytes = bb.second.second;
-      int rc = hip_check(r->ctx, hipMemcpyAsync(sl.h + w, col_get(o, f), bytes, hipMemcpyDeviceToHost, r->ctx->stream),
-                         "D2H row batch");
+    for (const Range& rg : rs) {
+      const int rc = hip_check(r->ctx, hipMemcpyAsync(sl.h + rg.hoff, rg.d, rg.bytes, hipMemcpyDeviceToHost,
+                                                      r->ctx->stream), "D2H row batch");
       if (rc) return r->fail_ctx(rc);
-      col_set(o, f, sl.h + w);  // the slab's view points at host memory
-      w += (bytes + 255) & ~(uint64_t)255;
     }
-    const int rc = sync_ctx(r->ctx);
+    for (const Buf& bf : bufs) {  // the slab's views point at host memory
+      const Range& rg = rs[bf.range];
+      col_set(sl.out[bf.col], bf.f, sl.h + rg.hoff + (uint64_t)(bf.d - rg.d));
+    }
+    const int rc = hip_check(r->ctx, hipStreamSynchronize(r->ctx->stream), "hipStreamSynchronize");
     return rc ? r->fail_ctx(rc) : ORCG_OK;
   }
   void run_job(uint64_t t) {
@@ -2221,6 +2448,19 @@ struct orcg_row_reader {
     int rc;
     std::string err;
     const double t0 = now_s();
+    // host work ahead, concurrently with this stripe's decode and copies:
+    // decompress stripe t + 1 into the other stage (stripe t - 1 is done
+    // with it); prepare reads only the file and this row reader's selection
+    std::thread ahead;
+    const uint64_t u = t + 1;
+    if (u < last && prepared[u & 1] != u) {
+      prepared[u & 1] = u;
+      ahead = std::thread([this, u] {
+        const double tp = now_s();
+        (void)r->prepare(u, stage[u & 1], selected);  // a failure is kept in the stage
+        addp(4, now_s() - tp);
+      });
+    }
     {
       std::lock_guard<std::mutex> lk(r->mu);
       orcg_reader::Active act(r, own, selected, lazy_dict);
@@ -2253,23 +2493,7 @@ struct orcg_row_reader {
       slab_state[t & 1] = 2;
     }
     cv.notify_all();
-    // host work ahead: decompress stripe t + 1 while the caller consumes
-    const uint64_t u = t + 1;
-    if (u < last && prepared[u & 1] != u) {
-      bool idle;
-      {
-        std::lock_guard<std::mutex> lk(m);
-        idle = jobs.empty() && !stop;
-      }
-      if (idle) {
-        const double tp = now_s();
-        std::lock_guard<std::mutex> lk(r->mu);
-        orcg_reader::Active act(r, own, selected, lazy_dict);
-        prepared[u & 1] = u;
-        (void)r->prepare(u, stage[u & 1]);  // a failure is kept in the stage
-        addp(4, now_s() - tp);
-      }
-    }
+    if (ahead.joinable()) ahead.join();
   }
   void loop() {
     for (;;) {
@@ -2529,8 +2753,21 @@ int orcg_reader_is_selected(const orcg_reader* r, uint32_t type_id) {
   return r && type_id < r->own_sel.size() && r->own_sel[type_id] ? 1 : 0;
 }
 
+// ReaderMetrics::ReaderCall / ReaderInclusiveLatencyUs around a caller-facing
+// call (the reference's SCOPED_STOPWATCH in RowReaderImpl::next, Reader.cc:1393)
+struct ReaderCallScope {
+  orcg_reader* r;
+  double t0 = now_s();
+  explicit ReaderCallScope(orcg_reader* rr) : r(rr) {}
+  ~ReaderCallScope() {
+    r->madd(orcg_reader::kMReaderCall, 1);
+    r->madd(orcg_reader::kMReaderLatency, (uint64_t)((now_s() - t0) * 1e6));
+  }
+};
+
 int orcg_reader_read_stripe(orcg_reader* r, uint64_t stripe) {
   if (!r) return ORCG_INVALID_ARGUMENT;
+  ReaderCallScope call(r);
   std::lock_guard<std::mutex> lk(r->mu);
   orcg_reader::Active act(r, r->own_ctx, r->own_sel, r->own_lazy);
   return r->read_stripes(stripe, 1);
@@ -2559,6 +2796,7 @@ int orcg_reader_bench_stripe_decode(orcg_reader* r, uint64_t stripe, uint32_t it
 
 int orcg_reader_read_stripes(orcg_reader* r, uint64_t first, uint64_t count) {
   if (!r) return ORCG_INVALID_ARGUMENT;
+  ReaderCallScope call(r);
   std::lock_guard<std::mutex> lk(r->mu);
   orcg_reader::Active act(r, r->own_ctx, r->own_sel, r->own_lazy);
   return r->read_stripes(first, count);
@@ -2654,6 +2892,7 @@ int orcg_row_reader_is_selected(const orcg_row_reader* rr, uint32_t type_id) {
 
 int orcg_row_reader_next(orcg_row_reader* rr, uint64_t capacity, uint64_t* rows) {
   if (!rr || !rows) return ORCG_INVALID_ARGUMENT;
+  ReaderCallScope call(rr->r);
   *rows = 0;
   std::fill(rr->in_batch.begin(), rr->in_batch.end(), 0);
   rr->batch_rows = 0;
@@ -2772,15 +3011,23 @@ uint64_t orcg_reader_last_batched_streams(const orcg_reader* r) { return r ? r->
 int orcg_reader_get_metrics(orcg_reader* r, orcg_reader_metrics* out) {
   if (!r || !out) return ORCG_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(r->mu);
-  static_assert(sizeof(orcg_reader_metrics) == sizeof(r->metrics), "orcg_reader_metrics layout");
-  memcpy(out, r->metrics, sizeof(r->metrics));
+  static_assert(sizeof(orcg_reader_metrics) == 14 * sizeof(uint64_t), "orcg_reader_metrics layout");
+  uint64_t* o = (uint64_t*)out;
+  for (int i = 0; i < 14; ++i) o[i] = r->metrics[i].load(std::memory_order_relaxed);
   return ORCG_OK;
 }
 
 int orcg_reader_reset_metrics(orcg_reader* r) {
   if (!r) return ORCG_INVALID_ARGUMENT;
   std::lock_guard<std::mutex> lk(r->mu);
-  memset(r->metrics, 0, sizeof(r->metrics));
+  for (auto& m : r->metrics) m.store(0, std::memory_order_relaxed);
+  return ORCG_OK;
+}
+
+int orcg_reader_set_metrics_timing(orcg_reader* r, int on) {
+  if (!r) return ORCG_INVALID_ARGUMENT;
+  std::lock_guard<std::mutex> lk(r->mu);
+  r->metrics_timing = on != 0;
   return ORCG_OK;
 }
 uint64_t orcg_reader_last_stage_bytes(const orcg_reader* r) { return r ? r->stage_bytes : 0; }

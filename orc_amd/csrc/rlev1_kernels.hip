@@ -198,6 +198,7 @@ __global__ __launch_bounds__(kV1Threads) void rlev1_kernel(const uint8_t* __rest
 
 #ifdef ORCG_PHASE_PROF
   uint64_t prof_last_ = wall_clock64();
+  const uint64_t prof_t0_ = prof_last_;
 #endif
   const int tid = (int)threadIdx.x;
   const int lane = tid % kWave, wave = tid / kWave;
@@ -583,6 +584,9 @@ __global__ __launch_bounds__(kV1Threads) void rlev1_kernel(const uint8_t* __rest
     const bool stop = s_ctl[2] != 0;
     __syncthreads();  // the window and the tables are rewritten by the next pass
     V1PROF_MARK(8);
+#ifdef ORCG_PHASE_PROF
+    if (threadIdx.x == 0) atomicMax(&g_v1phase[9], (unsigned long long)(wall_clock64() - prof_t0_));
+#endif
     vi += NV;
     if (stop) {
       stopped = true;

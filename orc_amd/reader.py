@@ -451,6 +451,12 @@ class Reader:
             check(self._L.orcg_reader_reset_metrics(self._h))
         return dict(zip(self.METRIC_NAMES, (int(x) for x in t)))
 
+    def set_metrics_timing(self, on=True):
+        """Time the integer-RLE and byte-RLE launches with HIP events
+        (DecodingLatencyUs / ByteDecodingLatencyUs; the reference fills its
+        metrics only when built with BUILD_CPP_ENABLE_METRICS)."""
+        check(self._L.orcg_reader_set_metrics_timing(self._h, int(bool(on))), self._err)
+
     def set_stream_batching(self, on=True):
         """Decode a stripe's host-countable RLEv2 streams with one launch per
         kernel instance (default) or one launch per stream."""

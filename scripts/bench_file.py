@@ -45,6 +45,10 @@ WORKLOADS = {
 }
 
 
+
+HBM_PEAK = 8.0e12      # B/s, MI355X HBM3E peak (the roofline denominator everywhere)
+COPY_CEILING = 6.0e12  # B/s, the best measured device copy on these boxes (profiles/r03, probe5)
+
 def view_bytes(v, kind, precision):
     """Device bytes of one decoded column view (the batch layout of
     include/orcg_reader.h)."""
@@ -419,14 +423,17 @@ def main():
                                              "host_plan_and_row_index": round(ph[2], 4), "h2d": round(ph[3], 4),
                                              "device_decode": round(ph[4], 4)},
             "device_decode_Mrows_per_s": round(my_rows / max(ph[4], 1e-9) / 1e6, 1),
-            # VERDICT r01 #5 target: (uploaded stream bytes + decoded bytes) / 6 TB/s
-            "device_roofline_s": round((stats["stage_bytes"] + dec_bytes) / 6e12, 5),
-            "device_vs_roofline": round(ph[4] / max((stats["stage_bytes"] + dec_bytes) / 6e12, 1e-12), 1),
+            # roofline: (uploaded stream bytes + decoded bytes) at the MI355X HBM peak
+            # (8 TB/s, MI355X_MICROARCH.md); the measured device copy (~6 TB/s) is a
+            # second column, never the denominator
+            "device_roofline_s": round((stats["stage_bytes"] + dec_bytes) / HBM_PEAK, 6),
+            "device_vs_roofline": round(ph[4] / max((stats["stage_bytes"] + dec_bytes) / HBM_PEAK, 1e-12), 1),
+            "device_vs_copy_ceiling": round(ph[4] / max((stats["stage_bytes"] + dec_bytes) / COPY_CEILING, 1e-12), 1),
             "rle_streams": stats,
             "device_decode_steady": None if steady is None else dict(
                 steady, Mrows_per_s=round(my_rows / max(steady["device_decode_s"], 1e-9) / 1e6, 1),
-                vs_roofline=round(steady["device_decode_s"] / max((stats["stage_bytes"] + dec_bytes) / 6e12, 1e-12),
-                                  1)),
+                vs_roofline=round(steady["device_decode_s"] / max((stats["stage_bytes"] + dec_bytes) / HBM_PEAK,
+                                                                  1e-12), 1)),
             "host_batch_copy_s": None if host is None else round(host, 3),
             "concat": concat,
             "multi_reader": multi,

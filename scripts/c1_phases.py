@@ -30,7 +30,8 @@ def main():
     names = ["setup", "window", "bitmap", "exits", "chain", "groups", "table", "literals", "runs"]
     wgs = int(sys.argv[1]) if len(sys.argv) > 1 else 22 * n
     print(json.dumps({"stripes": n, "workgroups": wgs,
-                      "phases_us_per_wg": {nm: round(pb[k] * 0.01 / wgs, 3) for k, nm in enumerate(names)}}))
+                      "phases_us_per_wg": {nm: round(pb[k] * 0.01 / wgs, 3) for k, nm in enumerate(names)},
+                      "slowest_window_us": round(pb[9] * 0.01, 3)}))
 
 
 if __name__ == "__main__":

@@ -275,3 +275,69 @@ def test_wide_short_runs_vs_oracle():
                 ctx.synchronize()
                 np.testing.assert_array_equal(o.cpu().numpy(), v[a:b])
     ctx.set_rlev2_variant(0)
+
+
+@pytest.mark.parametrize("bits", [7, 33, 64])
+@pytest.mark.parametrize("signed", [True, False])
+def test_value_parallel_expansion_vs_oracle(bits, signed):
+    """The dense expansion's value-parallel path (rlev2_tiled.hip dense_expand:
+    SHORT_REPEAT / DIRECT / constant-step DELTA runs of 17-256 values inside
+    dense segments, each value found by a binary search over the runs' first
+    values): short-run segments (SHORT_REPEAT runs of 3-10 values) with DIRECT
+    runs of 17-99 values of `bits`-bit values and constant-step DELTA runs
+    (11-99 values) interleaved, on every pinned variant, bit-exact against
+    the oracle (RleDecoderV2.cc:184-248, 372-435)."""
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(17 * bits + int(signed))
+    vals, kinds, lens = [], [], []
+    total = 0
+    while total < 300_000:
+        r = rng.random()
+        if r < 0.6:
+            k, L = 0, int(rng.integers(3, 11))
+            x = int(rng.integers(-300, 300)) if signed else int(rng.integers(0, 1 << 12))
+            v = [x] * L
+        elif r < 0.85:
+            k, L = 1, int(rng.integers(17, 100))
+            if bits == 64:
+                v = [int(x) for x in rng.integers(-(1 << 63), (1 << 63) - 1, size=L, dtype=np.int64)]
+                if not signed:
+                    v = [x & ((1 << 63) - 1) for x in v]
+            else:
+                hi = 1 << (bits - 1 if signed else bits)
+                v = [int(x) for x in rng.integers(-hi if signed else 0, hi, size=L)]
+        else:
+            k, L = 3, int(rng.integers(11, 100))
+            start = int(rng.integers(-10 ** 6, 10 ** 6)) if signed else int(rng.integers(10 ** 6, 2 * 10 ** 6))
+            step = int(rng.integers(-50, 50)) if signed else int(rng.integers(0, 50))
+            v = [start + step * i for i in range(L)]
+        vals += v
+        kinds.append(k)
+        lens.append(L)
+        total += L
+    v = np.array(vals, dtype=np.int64)
+    kinds = np.array(kinds, dtype=np.uint8)
+    lens = np.array(lens, dtype=np.uint32)
+    stride = 10_000
+    data, pos = _encode_with_positions(orc_amd, v, signed, kinds, lens, stride)
+    want = oracle.rlev2_decode(data.tobytes(), v.size, signed)
+    np.testing.assert_array_equal(want, v)
+    ctx = orc_amd.default_context(0)
+    d_src = torch.from_numpy(data).cuda()
+    d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+    try:
+        for variant in DENSE_VARIANTS + [1]:
+            ctx.set_rlev2_variant(variant)
+            out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, signed, out)
+            ctx.synchronize()
+            got = out.cpu().numpy()
+            if not np.array_equal(got, want):
+                i = int(np.flatnonzero(got != want)[0])
+                raise AssertionError("variant %d: first mismatch at %d: got %s want %s" % (
+                    variant, i, got[max(0, i - 4):i + 8].tolist(), want[max(0, i - 4):i + 8].tolist()))
+    finally:
+        ctx.set_rlev2_variant(0)

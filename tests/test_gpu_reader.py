@@ -106,21 +106,40 @@ def test_device_views_and_timings(ctx):
 
 def test_reader_metrics(ctx):
     """ReaderMetrics (Reader.hh:59-76) through orcg_reader_get_metrics: one
-    reader call and one I/O per stripe read, chunks inflated, RLE and byte-RLE
-    streams decoded, the stripes' row groups; cumulative until reset."""
+    reader call per caller-facing call (RowReaderImpl::next's stopwatch,
+    Reader.cc:1393), chunks inflated, RLE streams decoded, one I/O per stream
+    read and its page-in time, no row-group counts without search arguments,
+    no read-range cache; cumulative until reset."""
     r = orc_amd.Reader(path("demo-11-zlib.orc"), ctx)
     assert set(r.metrics().values()) == {0}
     r.read_stripes_device(0, 3)
     m = r.metrics()
-    assert m["ReaderCall"] == 3 and m["IOCount"] == 3
-    assert m["DecompressionCall"] > 0 and m["DecodingCall"] > 0
-    assert m["SelectedRowGroupCount"] == 3  # 5,000-row stripes, stride 10,000
+    assert m["ReaderCall"] == 1 and m["ReaderInclusiveLatencyUs"] > 0
+    assert m["DecompressionCall"] > 0 and m["DecompressionLatencyUs"] >= 0
+    assert m["DecodingCall"] == 3 * 13  # demo-11: 13 RLEv1 streams per stripe
+    assert m["IOCount"] == 3 * (13 + 4 + 1)  # its RLE streams, 4 dictionary blobs, the stripe footer
+    assert m["SelectedRowGroupCount"] == 0 and m["EvaluatedRowGroupCount"] == 0
+    assert m["ReadRangeCacheHits"] == 0 and m["ReadRangeCacheMisses"] == 0
     assert m["ReaderInclusiveLatencyUs"] >= m["DecodingLatencyUs"]
-    assert m["EvaluatedRowGroupCount"] == 0
     r.read_stripe(3)
     m2 = r.metrics(reset=True)
-    assert m2["ReaderCall"] == 4 and m2["DecodingCall"] > m["DecodingCall"]
+    assert m2["ReaderCall"] == 2 and m2["DecodingCall"] == 4 * 13
     assert set(r.metrics().values()) == {0}
+    # row reader: one call per next(); with event timing, device latencies of
+    # both decoder kinds (a file with PRESENT streams for the byte decoder)
+    r = orc_amd.Reader(path("nulls-at-end-snappy.orc"), ctx)
+    r.set_metrics_timing(True)
+    rr = r.create_row_reader()
+    b = rr.create_row_batch(1000)
+    calls = 0
+    while rr.next(b):
+        calls += 1
+    calls += 1  # the last call returns no rows
+    m = r.metrics()
+    assert m["ReaderCall"] == calls
+    assert m["ByteDecodingCall"] > 0 and m["ByteDecodingLatencyUs"] > 0
+    assert m["DecodingCall"] > 0 and m["DecodingLatencyUs"] > 0
+    assert m["IOCount"] > 0
 
 
 def test_in_memory_source_matches_file(ctx):

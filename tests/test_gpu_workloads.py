@@ -9,6 +9,10 @@ ORC C++, the file-level checker), column by column with numpy.
       Reference readers: IntegerColumnReader / Decimal64ColumnReader /
       StringDictionaryColumnReader / StringDirectColumnReader
       (c++/src/ColumnReader.cc:224-258, :1384-1527, :509-607, :615-793).
+  configs[2]: demo-12's schema tiled to ~7.7 M rows (4 tiles of its 1.92 M),
+      zlib, 4 MB stripes (>= 3 stripes): DELTA / DIRECT / SHORT_REPEAT
+      integer streams and DICTIONARY_V2 strings, every stripe compared
+      (TestMatch.cc:262-275 reads demo-12 whole).
   configs[4]: struct<a:list<int>, m:map<string,int>> with 10 % nulls at every
       level, zstd, row index on, >= 3 stripes. Reference readers:
       StructColumnReader / ListColumnReader / MapColumnReader
@@ -20,11 +24,12 @@ import pytest
 
 import orc_amd
 from file_parity import compare_stripe
-from workload_files import make_c4, make_c5
+from workload_files import make_c3, make_c4, make_c5
 
 pytestmark = pytest.mark.gpu
 
 ROWS = 2_000_000
+C3_ROWS = 4 * 1_920_800  # make_c3 tiles demo-12's 1,920,800 rows
 
 
 @pytest.fixture(scope="module")
@@ -36,6 +41,9 @@ def files(tmp_path_factory):
         p = os.path.join(str(d), name + ".orc")
         maker(p, ROWS, 8)
         out[name] = p
+    p = os.path.join(str(d), "c3.orc")
+    make_c3(p, C3_ROWS, 4)
+    out["c3"] = p
     return out
 
 
@@ -44,14 +52,14 @@ def ctx():
     return orc_amd.Context(0)
 
 
-@pytest.mark.parametrize("name", ["c4", "c5"])
+@pytest.mark.parametrize("name", ["c3", "c4", "c5"])
 def test_workload_every_stripe_matches_pyarrow(ctx, files, name):
     import pyarrow.orc as po
 
     path = files[name]
     r = orc_amd.Reader(path, ctx)
     f = po.ORCFile(path)
-    assert r.num_rows == ROWS and r.num_stripes >= 3, (r.num_rows, r.num_stripes)
+    assert r.num_rows == (C3_ROWS if name == "c3" else ROWS) and r.num_stripes >= 3, (r.num_rows, r.num_stripes)
     for s in range(r.num_stripes):
         b = r.read_stripe(s)
         compare_stripe(r, b, f.read_stripe(s), "%s stripe %d" % (name, s))
