@@ -636,6 +636,25 @@ int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_f
   return hip_check(ctx, hipGetLastError(), "flag launch");
 }
 
+// A small host -> device copy by the shader: the workgroups read the pinned,
+// device-mapped source over PCIe and store to HBM. For the tens of KB of a
+// small stripe's staging this starts sooner than a DMA-engine copy, whose
+// hand-off to the compute queue cost ~15-20 us per stripe on configs[0].
+__global__ __launch_bounds__(256) void pull_kernel(const u4* __restrict__ src, u4* __restrict__ dst, uint64_t n16) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256)
+    dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+int launch_pull(Ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes) {
+  if (bytes == 0) return ORCG_OK;
+  if (((uintptr_t)d_dst | (uintptr_t)h_src) & 15u)
+    return set_error(ctx, ORCG_INVALID_ARGUMENT, "pull copy needs 16-byte aligned buffers");
+  const uint64_t n16 = (bytes + 15) / 16;  // (the staging is allocated past whole 16-byte words)
+  const unsigned grid = (unsigned)std::min<uint64_t>((n16 + 1023) / 1024, 128);
+  hipLaunchKernelGGL(pull_kernel, dim3(grid), dim3(256), 0, ctx->stream, (const u4*)h_src, (u4*)d_dst, n16);
+  return hip_check(ctx, hipGetLastError(), "pull launch");
+}
+
 int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out) {
   if (n == 0) return ORCG_OK;
   const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256 * 32);

@@ -254,6 +254,9 @@ int launch_count_nonzero(Ctx* ctx, const uint8_t* d_nn, uint64_t n, uint64_t* d_
 int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_flag);
 enum WidenKind { kWidenI8 = 0, kWidenU8 = 1, kWidenF32 = 2 };
 int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out);
+// Host (pinned, device-mapped) -> device copy by a kernel on ctx->stream;
+// both buffers 16-byte aligned, rounded up to whole 16-byte words.
+int launch_pull(Ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes);
 
 // Dispatch on ctx->rlev2_variant.
 inline int launch_rlev2(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,

@@ -233,6 +233,7 @@ struct HostStage {
   // and job arena, upload_tail_bytes): upload_and_decode never reallocates
   uint64_t slack = 0;
   ~HostStage() { pinned_free(h); }
+  bool pinned_mapped = false;  // h is hipHostMalloc'd (the device can read it through the same pointer)
   bool ensure(uint64_t bytes, uint64_t keep) {
     if (bytes <= cap) return true;
     const uint64_t ncap = std::max<uint64_t>(bytes + (bytes >> 2), 1 << 20) + slack;
@@ -244,6 +245,7 @@ struct HostStage {
     }
     h = nh;
     cap = ncap;
+    pinned_mapped = ncap < (size_t(8) << 20);  // pinned_alloc's hipHostMalloc range
     return true;
   }
   int fail(int status, const std::string& m) {
@@ -2045,8 +2047,17 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   }
   const uint64_t up = arena_off + ctx->arena_used;
   stage_bytes += up;
-  // (uploaded even after a failure above: finish() reads the records back)
-  const int urc = hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, up, hipMemcpyHostToDevice, ctx->stream), "H2D stripe");
+  // (uploaded even after a failure above: finish() reads the records back);
+  // a small stripe (configs[0]: ~60 KB) is pulled by a kernel from the
+  // pinned staging, a large one copied by the DMA engine
+  static const uint64_t pull_max = [] {
+    const char* e = getenv("ORCG_PULL_BYTES");  // A/B: 0 = always the DMA copy
+    return e ? strtoull(e, nullptr, 10) : (uint64_t)(256u << 10);
+  }();
+  const int urc = up <= pull_max && hs.pinned_mapped
+                      ? launch_pull(ctx, ds.d_stage, hs.h, up)
+                      : hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, up, hipMemcpyHostToDevice, ctx->stream),
+                                  "H2D stripe");
   if (urc && !rc) rc = fail_ctx(urc);
   fl.t1 = now_s();
   if (!rc && !launches.empty() && (rc = timed(0, [&]() -> int { return run_multi(ctx, launches); })))

@@ -23,6 +23,7 @@ using namespace dev;
 constexpr int kV1Threads = 256;
 constexpr uint32_t kV1Tail = 1536;  // >= the longest group of <= 10-byte varints (1 + 128 * 10)
 constexpr uint32_t kNone = 0xffffu;
+constexpr uint32_t kLaneRun = 32;  // runs up to this many values expand on one lane
 
 typedef uint32_t v1u4 __attribute__((ext_vector_type(4)));
 
@@ -187,8 +188,9 @@ __global__ __launch_bounds__(kV1Threads) void rlev1_kernel(const uint8_t* __rest
   __shared__ uint16_t s_gpos[G::kMaxGroups + 1];
   __shared__ uint64_t s_gmeta[G::kMaxGroups + 1];
   __shared__ uint32_t s_wsum[3][kV1Threads / kWave];
-  // [0] next window start, [1] incomplete group + 1, [2] stop, [3] -
+  // [0] next window start, [1] incomplete group + 1, [2] stop, [3] long runs
   __shared__ uint32_t s_ctl[4];
+  __shared__ uint16_t s_rlong[G::kMaxRuns];  // the window's runs of more than kLaneRun values
   static_assert(G::kMaxRuns * 8 <= kWin * 2 && G::kMaxRuns * 8 <= 4 * kChunk, "run tables");
   uint32_t* const s_win = s_winbuf + 4;
   uint16_t* s_exit2 = s_exit + kChunk;
@@ -482,6 +484,7 @@ __global__ __launch_bounds__(kV1Threads) void rlev1_kernel(const uint8_t* __rest
               if (sh < 64) acc |= (uint64_t)(s_bytes[bb] & 0x7fu) << sh;
             s_rbase[rr] = sg ? unzigzag(acc) : acc;
             s_rmeta[rr] = (uint64_t)d | ((uint64_t)(hb + 3u) << 32) | ((delta & 0xffu) << 48);
+            if (hb + 3u > kLaneRun) s_rlong[atomicAdd(&s_ctl[3], 1u)] = (uint16_t)rr;
             ++rr;
           }
           ++k;
@@ -571,12 +574,25 @@ __global__ __launch_bounds__(kV1Threads) void rlev1_kernel(const uint8_t* __rest
       }
     }
     V1PROF_MARK(7);
-    // 5. runs: one wave per run, base + j * delta on lane j
-    for (uint32_t r = (uint32_t)wave; r < NR; r += kV1Threads / kWave) {
+    // 5. runs: a short run (<= kLaneRun values) on one lane, a long one on
+    // a whole wave (base + j * delta on lane j); the long ones were listed
+    // by the table step
+    for (uint32_t r = (uint32_t)tid; r < NR; r += kV1Threads) {
+      const uint64_t m = s_rmeta[r];
+      const uint32_t L = (uint32_t)(m >> 32) & 0xffu;
+      if (L > kLaneRun) continue;
+      const uint64_t base = s_rbase[r];
+      const uint64_t v0 = vi + (uint32_t)m;
+      const uint64_t delta = (uint64_t)(int64_t)(int8_t)(uint8_t)(m >> 48);
+      for (uint32_t j = 0; j < L; ++j) put_v(dst, v0 + j, S.begin, vend, base + (uint64_t)j * delta);
+    }
+    const uint32_t nlong = s_ctl[3];
+    for (uint32_t q = (uint32_t)wave; q < nlong; q += kV1Threads / kWave) {
+      const uint32_t r = uni(s_rlong[q]);
       const uint64_t m = s_rmeta[r];
       const uint64_t base = s_rbase[r];
       const uint64_t v0 = vi + (uint32_t)m;
-      if (v0 >= vend) break;
+      if (v0 >= vend) continue;
       const uint32_t L = (uint32_t)(m >> 32) & 0xffu;
       const uint64_t delta = (uint64_t)(int64_t)(int8_t)(uint8_t)(m >> 48);
       for (uint32_t j = (uint32_t)lane; j < L; j += kWave) put_v(dst, v0 + j, S.begin, vend, base + (uint64_t)j * delta);
