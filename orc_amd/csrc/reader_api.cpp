@@ -413,6 +413,10 @@ struct orcg_reader {
     size_t h_rb_cap = 0, rb_words = 0, rb_used = 0;
     std::vector<EvPair> ev_used;  // metrics timing events
     hipEvent_t done = nullptr;    // recorded after the read-back copy
+    // GPU-time split of the flight (timings[3] / [4]): before and after the
+    // stripe's upload, and after its last decode launch
+    hipEvent_t ev_up0 = nullptr, ev_up1 = nullptr, ev_dec = nullptr;
+    bool ev_split = false;
     bool enqueued = false;        // done / the read-back copy belong to this issue
     int rc = ORCG_OK;             // the inline (host-detected) failure of the issue
     uint32_t err_col = 0;
@@ -480,6 +484,8 @@ struct orcg_reader {
       if (f.h_rb) (void)hipHostFree(f.h_rb);
       for (const EvPair& p : f.ev_used) ev_pool.push_back(p.a), ev_pool.push_back(p.b);
       if (f.done) (void)hipEventDestroy(f.done);
+      for (hipEvent_t e : {f.ev_up0, f.ev_up1, f.ev_dec})
+        if (e) (void)hipEventDestroy(e);
     }
     for (hipEvent_t e : ev_pool) (void)hipEventDestroy(e);
   }
@@ -571,14 +577,22 @@ struct orcg_reader {
   uint64_t cur_n = 0;
   const uint8_t* cur_in_nn = nullptr;
   const uint8_t* cur_row_nn = nullptr;
+  // segments(): the row-group prefix it built the table from (a masked
+  // row-index stream), else null; with the mask it places the stream's
+  // values at their rows inside the decode (RowScatter)
+  const int64_t* seg_prefix = nullptr;
+  const uint8_t* seg_mask = nullptr;
   int segments(Col& c, int slot, bool boolean, const uint64_t** d_seg, uint64_t* nseg);
+  bool fused_place() const;
   // RLE integer stream: v1 for DIRECT / DICTIONARY encodings (convertRleVersion,
   // DictionaryLoader.hh:42) unless force_v2 (Decimal64ColumnReaderV2 is always RLEv2)
   // (*out: the stream's values, decoded by this stripe's multi-stream batch
   // when collect() queued it, else allocated and decoded now)
   // (dcount: the value count on the device, `count` then only sizes the output)
+  // (placed, may be null: when the decode can place the values at the rows
+  // of cur_row_nn itself, *placed = those cur_n rows (null rows 0), else null)
   int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** out, bool force_v2 = false,
-                 const uint64_t* dcount = nullptr);
+                 const uint64_t* dcount = nullptr, int64_t** placed = nullptr);
   // Multi-stream batch: before decode(), the RLEv2 streams whose value
   // counts and segments are known without device results (columns with no
   // PRESENT stream, under parents with none) are queued and decoded by one
@@ -604,7 +618,7 @@ struct orcg_reader {
   int queue_dict(uint32_t id, uint64_t n);
   int collect(uint32_t id, uint64_t n, const int64_t* rg_rows);
   int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones = nullptr,
-                  const uint64_t* d_count = nullptr);
+                  const uint64_t* d_count = nullptr, uint8_t* place_out = nullptr, bool* placed = nullptr);
   int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
   template <typename T>
   T* alloc(uint64_t count) {
@@ -680,6 +694,8 @@ int orcg_reader::scatter(const void* dense, const uint8_t* nn, uint64_t n, void*
 // at each row group's first row (PRESENT streams count the incoming rows).
 int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg, uint64_t* nseg) {
   StreamBuf& sb = c.s[slot];
+  seg_prefix = nullptr;
+  seg_mask = nullptr;
   if (!sb.pos) {
     *d_seg = (const uint64_t*)(D->d_stage + sb.seg_off);
     *nseg = sb.plan->segs.size();
@@ -695,6 +711,8 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
     ORCG_ALLOC(int64_t, pre, G + 1);
     if ((rc = launch_rg_prefix(ctx, mask, cur_n, cur_rows, G, counts, pre))) return fail_ctx(rc);
     prefix = pre;
+    seg_prefix = pre;
+    seg_mask = mask;
   }
   ORCG_ALLOC(uint64_t, seg, 2 * G);
   if ((rc = launch_rg_segtab(ctx, (const int64_t*)(D->d_stage + sb.rg_off), prefix, G, boolean, seg)))
@@ -733,8 +751,22 @@ bool orcg_reader::device_work(uint32_t id) const {
   return true;
 }
 
+// After segments(): the decode can place its values at the rows itself.
+// Off unless ORCG_FUSED_PLACE=1: the row-group segment kernels run one
+// workgroup per row group, and placing inside them costs those launches
+// about what the separate full-chip scatter costs (configs[4]: 3.12-3.26 ms
+// fused vs 3.06-3.11 ms separate, profiles/r05/bench_file_c5_place_ab.json).
+bool orcg_reader::fused_place() const {
+  static const bool on = [] {
+    const char* e = getenv("ORCG_FUSED_PLACE");
+    return e && atoi(e) != 0;
+  }();
+  return on && seg_prefix && seg_mask && cur_rows && H->ngroups;
+}
+
 int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** pout, bool force_v2,
-                            const uint64_t* dcount) {
+                            const uint64_t* dcount, int64_t** placed) {
+  if (placed) *placed = nullptr;
   const uint64_t key = (uint64_t)(&c - H->cols.data()) * 8 + (uint64_t)slot;
   const auto it = batched.find(key);
   if (it != batched.end() && it->second.second == count) {
@@ -759,11 +791,26 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   int rc = segments(c, slot, false, &d_seg, &nseg);
   if (rc) return rc;
   const int sg = is_signed ? 1 : 0;
+  // the values placed at the rows of the column's mask by the decode itself
+  RowScatter rsc{};
+  const bool place = placed && !v1 && ctx->rlev2_variant != ORCG_RLEV2_WAVE_WALK && fused_place() &&
+                     seg_mask == cur_row_nn;
+  static const bool dbg = getenv("ORCG_DEBUG_PLACE") != nullptr;
+  if (dbg && placed)
+    fprintf(stderr, "place: column %u slot %d v1 %d row index %d prefix %d -> %s\n", (unsigned)(&c - H->cols.data()),
+            slot, v1 ? 1 : 0, sb.pos ? 1 : 0, seg_prefix ? 1 : 0, place ? "fused" : "scatter");
+  if (place) {
+    int64_t* rows_out = alloc<int64_t>(cur_n);
+    if (!rows_out) return fail_oom(__LINE__);
+    rsc = RowScatter{seg_mask, cur_rows, seg_prefix, cur_n, H->ngroups, rows_out};
+    *placed = rows_out;
+  }
   madd(kMDecodeCall, 1);
   rc = timed(0, [&]() -> int {
     if (v1) return launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
-    return dcount ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, dcount)
-                  : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
+    return dcount || place ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, dcount,
+                                                place ? &rsc : nullptr)
+                           : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
   });
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
@@ -911,8 +958,9 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
 }
 
 int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones,
-                             const uint64_t* d_count) {
+                             const uint64_t* d_count, uint8_t* place_out, bool* placed) {
   StreamBuf& sb = c.s[slot];
+  if (placed) *placed = false;
   if (count == 0) return ORCG_OK;
   if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
   if (!sb.pos && !d_count) {  // (with a device count the kernel reports a short stream)
@@ -926,9 +974,17 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   uint64_t nseg;
   int rc = segments(c, slot, boolean, &d_seg, &nseg);
   if (rc) return rc;
+  // placed at the rows of the incoming mask by the decode itself
+  RowScatter rsc{};
+  const bool place = place_out && slot == kSlotPresent && fused_place() && seg_mask == cur_in_nn;
+  if (place) {
+    rsc = RowScatter{seg_mask, cur_rows, seg_prefix, cur_n, H->ngroups, place_out};
+    *placed = true;
+  }
   madd(kMByteCall, 1);
   rc = timed(1, [&]() -> int {
-    return launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count);
+    return launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count,
+                          place ? &rsc : nullptr);
   });
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
@@ -973,10 +1029,14 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     // the decode counts the set rows it writes: the non-null rows, with or
     // without the parent's mask scattered in
     uint64_t* ones = D->d_ones + id;
-    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits, ones, d_in))) return rc;
+    uint8_t* placed_nn = nullptr;
+    if (in_nn) ORCG_ALLOC_TO(uint8_t, placed_nn, n);
+    bool placed = false;
+    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits, ones, d_in, placed_nn, &placed)))
+      return rc;
     if (in_nn) {
-      ORCG_ALLOC_TO(uint8_t, nn, n);
-      if ((rc = scatter(bits, in_nn, n, nn, 1))) return fail_ctx(rc);
+      nn = placed_nn;
+      if (!placed && (rc = scatter(bits, in_nn, n, nn, 1))) return fail_ctx(rc);
     } else {
       nn = bits;
     }
@@ -1037,9 +1097,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (decimal_as_long && t.precision - 1u < 18u) {  // precision 1..18 (0 = Hive 0.11 first)
       // Decimal64ColumnReaderV2 (ColumnReader.cc:1529-1576): RLEv2 unscaled values
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64V2 column. ColumnId=" + cid);
-      int64_t* dense;
-      if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, true))) return rc;
-      if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
+      int64_t *dense, *placed;
+      if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, true, nullptr, row_nn ? &placed : nullptr))) return rc;
+      if (!(c.data = row_nn && placed ? placed : place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
     } else {
       // Decimal64ColumnReader / Decimal128ColumnReader (:1384-1527): varint
       // DATA, per-value scales in SECONDARY (signed RLE)
@@ -1119,9 +1179,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (!(c.data = place_i64(secs)) || !(c.secondary = place_i64(nanos))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (is_int_kind(k)) {
     if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Integer column");
-    int64_t* dense;
-    if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, false, d_nonnull))) return rc;
-    if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
+    int64_t *dense, *placed;
+    if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, false, d_nonnull, row_nn ? &placed : nullptr))) return rc;
+    if (!(c.data = row_nn && placed ? placed : place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (k == ORCG_TYPE_BOOLEAN || k == ORCG_TYPE_BYTE) {
     if (!has_data)
       return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_BOOLEAN ? "DATA stream not found in Boolean column"
@@ -1221,10 +1281,13 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       });
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDictionaryColumn");
       c.blob = db.present ? D->d_stage + db.host_off : nullptr;
-      int64_t* idx;
-      if ((rc = int_stream(c, kSlotData, false, nonnull, &idx, false, d_nonnull))) return rc;
+      int64_t *idx, *placed;
+      if ((rc = int_stream(c, kSlotData, false, nonnull, &idx, false, d_nonnull, row_nn ? &placed : nullptr)))
+        return rc;
       int64_t* ridx = idx;
-      if (row_nn) {
+      if (row_nn && placed) {
+        ridx = placed;
+      } else if (row_nn) {
         ORCG_ALLOC_TO(int64_t, ridx, n);
         if ((rc = scatter(idx, row_nn, n, ridx, 8))) return fail_ctx(rc);
       }
@@ -1242,20 +1305,28 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     } else {
       if (!has_len) return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDirectColumn");
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDirectColumn");
-      int64_t* dlen;
-      if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen))) return rc;
-      ORCG_ALLOC(int64_t, dstart, nonnull + 1);
-      if ((rc = launch_exclusive_scan(ctx, dlen, nonnull, dstart))) return fail_ctx(rc);
+      int64_t *dlen, *placed;
+      if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false, nullptr, row_nn ? &placed : nullptr)))
+        return rc;
+      // lengths placed at the rows by the decode (null rows 0): the scan over
+      // the rows gives every row its start (a null row's is its successor's)
+      const bool rows_placed = row_nn && placed;
+      const uint64_t ns = rows_placed ? n : nonnull;
+      ORCG_ALLOC(int64_t, dstart, ns + 1);
+      if ((rc = launch_exclusive_scan(ctx, rows_placed ? placed : dlen, ns, dstart))) return fail_ctx(rc);
       StreamBuf& db = c.s[kSlotData];
       c.blob = D->d_stage + db.host_off;
       c.blob_len = db.len;
-      const uint64_t* need = defer(dstart + nonnull, 1);
+      const uint64_t* need = defer(dstart + ns, 1);
       if (!need) return fail(ORCG_DEVICE_ERROR, "D2H of the string bytes failed");
       const uint64_t blob_len = c.blob_len;
       F->checks.emplace_back(cur_col, [this, need, blob_len]() -> int {
         return *need > blob_len ? fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next") : ORCG_OK;
       });
-      if (row_nn) {
+      if (rows_placed) {
+        start = dstart;
+        len = placed;
+      } else if (row_nn) {
         if ((rc = scatter(dstart, row_nn, n, start, 8))) return fail_ctx(rc);
         if ((rc = scatter(dlen, row_nn, n, len, 8))) return fail_ctx(rc);
       } else {
@@ -1269,10 +1340,13 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (!has_len)
       return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_LIST ? "LENGTH stream not found in List column"
                                                         : "LENGTH stream not found in Map column");
-    int64_t* dlen;
-    if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false, d_nonnull))) return rc;
+    int64_t *dlen, *placed;
+    if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false, d_nonnull, row_nn ? &placed : nullptr)))
+      return rc;
     int64_t* rlen = dlen;
-    if (row_nn) {
+    if (row_nn && placed) {
+      rlen = placed;
+    } else if (row_nn) {
       ORCG_ALLOC_TO(int64_t, rlen, n);
       if ((rc = scatter(dlen, row_nn, n, rlen, 8))) return fail_ctx(rc);
     }
@@ -1997,6 +2071,9 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
     fl.done = nullptr;
     return early(fail(ORCG_DEVICE_ERROR, "event creation failed"));
   }
+  for (hipEvent_t* e : {&fl.ev_up0, &fl.ev_up1, &fl.ev_dec})
+    if (!*e && hipEventCreate(e) != hipSuccess) *e = nullptr;
+  fl.ev_split = fl.ev_up0 && fl.ev_up1 && fl.ev_dec;
   const size_t need_defer = 4 * nc + 16;
   if (fl.defer_cap < need_defer) {
     if (fl.h_defer) (void)hipHostFree(fl.h_defer);
@@ -2054,11 +2131,13 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
     const char* e = getenv("ORCG_PULL_BYTES");  // A/B: 0 = always the DMA copy
     return e ? strtoull(e, nullptr, 10) : (uint64_t)(256u << 10);
   }();
+  if (fl.ev_split && hipEventRecord(fl.ev_up0, ctx->stream) != hipSuccess) fl.ev_split = false;
   const int urc = up <= pull_max && hs.pinned_mapped
                       ? launch_pull(ctx, ds.d_stage, hs.h, up)
                       : hip_check(ctx, hipMemcpyAsync(ds.d_stage, hs.h, up, hipMemcpyHostToDevice, ctx->stream),
                                   "H2D stripe");
   if (urc && !rc) rc = fail_ctx(urc);
+  if (fl.ev_split && hipEventRecord(fl.ev_up1, ctx->stream) != hipSuccess) fl.ev_split = false;
   fl.t1 = now_s();
   if (!rc && !launches.empty() && (rc = timed(0, [&]() -> int { return run_multi(ctx, launches); })))
     rc = fail_ctx(rc);
@@ -2067,6 +2146,7 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   fl.rc = rc;
   fl.err_col = err_col;
   fl.err_msg = last_error;
+  if (fl.ev_split && hipEventRecord(fl.ev_dec, ctx->stream) != hipSuccess) fl.ev_split = false;
   // the read-back copy, then the flight's event (queued copies land before
   // the buffers are reused)
   if (hipMemcpyAsync(fl.h_rb, ds.d_rb, 8 * fl.rb_used, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
@@ -2128,8 +2208,18 @@ int orcg_reader::finish(Flight& fl) {
   H = nullptr;
   D = nullptr;
   const double t_end = now_s();
-  timings[3] += fl.t1 - fl.t0;
-  timings[4] += t_end - fl.t1;
+  // the upload's and the decode's GPU time (the flight's events, complete
+  // here: first_error waited for `done`); host clocks without them
+  float up_ms = 0, dec_ms = 0;
+  if (fl.ev_split && hipEventElapsedTime(&up_ms, fl.ev_up0, fl.ev_up1) == hipSuccess &&
+      hipEventElapsedTime(&dec_ms, fl.ev_up1, fl.ev_dec) == hipSuccess) {
+    timings[3] += up_ms * 1e-3;
+    timings[4] += dec_ms * 1e-3;
+  } else {
+    (void)hipGetLastError();
+    timings[3] += fl.t1 - fl.t0;
+    timings[4] += t_end - fl.t1;
+  }
   // ReaderMetrics (ReaderCall / ReaderInclusiveLatencyUs are counted per
   // caller-facing call: orcg_reader_read_stripe(s), orcg_row_reader_next):
   // the stripe's decompression, I/O and decode work
@@ -2486,12 +2576,18 @@ struct orcg_row_reader {
       if (rc) err = hs.err;
       const double t1 = now_s();
       if (!rc) {
+        const double g3 = r->timings[3], g4 = r->timings[4];
         rc = r->upload_and_decode(hs, *dev);
         const double t2 = now_s();
         if (!rc) rc = copy_out(sl);
         if (rc) err = r->last_error;
         addp(1, t2 - t1);
         addp(2, now_s() - t2);
+        static const bool dbg = getenv("ORCG_DEBUG_ROWREADER") != nullptr;
+        if (dbg)
+          fprintf(stderr, "row reader stripe %llu: prepare %.2f ms, upload+decode %.2f ms (GPU upload %.2f, decode %.2f), "
+                  "D2H %.2f ms\n", (unsigned long long)t, (t1 - t0) * 1e3, (t2 - t1) * 1e3,
+                  (r->timings[3] - g3) * 1e3, (r->timings[4] - g4) * 1e3, (now_s() - t2) * 1e3);
       }
       addp(0, t1 - t0);
       prepared[t & 1] = ~0ull;  // the stage is reused by stripe t + 2
@@ -2891,6 +2987,19 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
   rr->begin.assign(nt, 0);
   rr->count.assign(nt, 0);
   rr->in_batch.assign(nt, 0);
+  // the first stripe's decode starts now, on the worker, so the process's
+  // first-use costs (code objects, device and pinned allocations: ~40 ms on
+  // configs[4]) overlap the caller's setup instead of its first next()
+  // (ORCG_ROWREADER_PREFETCH=0: start at the first next(), as the
+  // reference's RowReaderImpl::startNextStripe does)
+  static const bool prefetch = [] {
+    const char* e = getenv("ORCG_ROWREADER_PREFETCH");
+    return !e || atoi(e) != 0;
+  }();
+  if (prefetch && rr->first < rr->last) {
+    std::unique_lock<std::mutex> lk(rr->m);
+    rr->post(lk, rr->first);
+  }
   *out = rr.release();
   return ORCG_OK;
 }

@@ -1599,7 +1599,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint64_t* __restrict__ p_segtab, uint64_t p_nsegs, uint64_t rows_per_group,
     uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* p_err,
     unsigned long long* __restrict__ defer_q, uint32_t defer_par, const RleJob* __restrict__ jobs,
-    uint32_t njobs, const uint64_t* __restrict__ p_dcount) {
+    uint32_t njobs, const uint64_t* __restrict__ p_dcount, const RowScatter rsc) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
@@ -1610,6 +1610,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   constexpr uint32_t kWinS = kUnion ? kWin + (uint32_t)(kWaves * kStage * 8 + kSlab / 8) : kWin;
   constexpr uint32_t kChunkS = kWinS - kMaxRun;
   static_assert(!kUnion || (kWin + 32) % 8 == 0, "stage alignment");
+  static_assert(kWinS + 32 >= kScatterLds, "the window holds the RowScatter tables");
   static_assert(!kDense || kChunk % kSlab == 0, "dense window chunk must be whole slabs");
   constexpr int kBufs = kPipe ? 2 : 1;
   static_assert(!(kDense && kPipe), "dense mode is a non-pipelined instance");
@@ -1703,6 +1704,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     return gg - uni64(J->seg_base);
   };
 
+  // (kDefer = 1: the segment was queued for the drain, which places it)
+  bool seg_queued = false;
   // one segment, from its start or (queued) from a byte offset / value index
   auto run_segment = [&](const uint64_t gg, const bool queued, const uint64_t q_pos, const uint64_t q_vi) {
   const uint64_t g = bind(gg);
@@ -2039,6 +2042,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               if (__hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned long long)defer_par)
                 __hip_atomic_store(any, (unsigned long long)defer_par, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
+            seg_queued = true;
             return;
           }
         }
@@ -2108,6 +2112,20 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   if (tid == 0 && v_next == ~0ull && vi < value_end) report(err, vi, kErrBadRead);  // stream ended early
   };
 
+  // RowScatter placement of single-stream segment g once it is decoded:
+  // its values [segtab value index, the next segment's) go to their rows
+  auto place = [&](const uint64_t g) {
+    if constexpr (!kMulti && !kPositions) {
+      if (!rsc.out) return;
+      uint64_t v1 = g + 1 < p_nsegs ? p_segtab[2 * (g + 1) + 1] : value_end;
+      if (v1 > value_end) v1 = value_end;
+      uint64_t v0 = p_segtab[2 * g + 1];
+      if (v0 > v1) v0 = v1;
+      __syncthreads();  // the workgroup's value stores, and its last use of s_win
+      scatter_rows<T>(rsc, p_dst, v0, v1, g, s_win[0]);
+    }
+  };
+
   if constexpr (kDefer == 2) {
     // the drain: workgroup w takes the contiguous share [w C, (w + 1) C) of
     // the launch's segments, finds the ones the serial launch stamped with
@@ -2132,6 +2150,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         for (unsigned long long f = uni64(s_flags[w]); f; f &= f - 1) {
           const uint64_t q = b + (uint64_t)(w * kWave + __builtin_ctzll(f));
           run_segment(q, true, uni64(defer_q[3 * q + 1]), uni64(defer_q[3 * q + 2]));
+          place(q);
           __syncthreads();  // LDS is reused by the next segment
         }
       }
@@ -2141,6 +2160,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     // (one call site per instance: a second one makes the compiler outline
     // run_segment into a call with a ~700-byte stack frame)
     run_segment(blockIdx.x, false, 0, 0);
+    if (!seg_queued) place(blockIdx.x);
   }
 }
 
@@ -2223,8 +2243,13 @@ static void debug_defer(Ctx* ctx, const unsigned long long* dq, uint64_t nsegs, 
 static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode, uint64_t rows_per_group,
                         uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes, const RleJob* jobs_d,
-                        uint32_t njobs_d, const uint64_t* dcount = nullptr) {
+                        uint32_t njobs_d, const uint64_t* dcount = nullptr, const RowScatter* rsc_p = nullptr) {
   if (nsegs == 0 || nvalues == 0) return ORCG_OK;
+  const RowScatter rsc = rsc_p ? *rsc_p : RowScatter{};
+  if (rsc.out && (jobs_d || positions_mode || value_begin))
+    return set_error(ctx, ORCG_INVALID_ARGUMENT, "row placement needs a single-stream segment-table launch");
+  if (rsc.out && ((uintptr_t)rsc.mask & 15u))
+    return set_error(ctx, ORCG_INVALID_ARGUMENT, "row placement needs a 16-byte aligned mask");
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   if (dst_bytes != 8 && dst_bytes != 4 && dst_bytes != 2)
     return set_error(ctx, ORCG_INVALID_ARGUMENT, "dst_bytes must be 8, 4 or 2");
@@ -2246,7 +2271,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
   hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
                      d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
-                     ctx->d_err, dq, dpar, jobs_d, njobs_d, dcount)
+                     ctx->d_err, dq, dpar, jobs_d, njobs_d, dcount, rsc)
 // single-stream instances (+ the multi-stream one for the default's
 // instances, ORCG_KX; the tuning variants have none, ORCG_KX1)
 #define ORCG_KX1(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                 \
@@ -2354,11 +2379,11 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
-                       int dst_bytes, const uint64_t* d_count) {
+                       int dst_bytes, const uint64_t* d_count, const RowScatter* rsc) {
   int variant = ctx->rlev2_variant;
   if (variant == 0) variant = default_variant(src_len, positions_mode ? nsegs * rows_per_group : nvalues);
   return launch_tiled(ctx, variant, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode, rows_per_group,
-                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count);
+                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count, rsc);
 }
 
 // Job tables go through a pinned ring mirrored on the device (entries are
