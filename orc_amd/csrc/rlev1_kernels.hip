@@ -160,7 +160,11 @@ __device__ __forceinline__ void seg_bounds(const uint64_t* segtab, const int64_t
 //   4. literal values: each thread streams the varints ending in its chunk
 //      out of registers (a varint begun earlier resumed from the 16 bytes
 //      before), consecutive values on consecutive chunks;
-//   5. runs: one wave per run, base + j * delta on lane j.
+//   5. runs: up to kLaneRun values one lane per run (consecutive runs on
+//      consecutive lanes: a column of short runs, e.g. 500 runs of 10, costs
+//      a few store rounds instead of one wave round per run), longer ones one
+//      wave per run, base + j * delta on lane j (their indices listed while
+//      the run table is written).
 // Errors keep the serial decoder's order: a group truncated by the stream's
 // end reports at its first value it cannot produce (the reference throws
 // from readByte when that value is requested), with atomicMin on the record.
