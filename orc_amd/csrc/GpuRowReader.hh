@@ -145,14 +145,28 @@ class DataBuffer {
 // The copies of one batch, spread over the calling thread and a few helper
 // threads that spin between batches (a batch of 1,024 rows is ~10-30 us of
 // copying; waking sleeping threads per batch would cost more than it saves)
-// and sleep after ~50 us without work.
+// and sleep after ~50 us without work. Besides byte copies a task can build a
+// string column's data pointers (the per-row work of StringVectorBatch).
 class CopyPool {
  public:
   struct Task {
     void* dst;
     const void* src;
-    uint64_t bytes;
+    uint64_t bytes;              // kind 0: bytes to copy; kind 1: rows
+    int kind = 0;                // 0 memcpy; 1 dst[i] = base + (len[i] > 0 ? src[i] - shift : 0)
+    const int64_t* len = nullptr;
+    char* base = nullptr;
+    int64_t shift = 0;
   };
+  static void exec(const Task& t) {
+    if (t.kind == 0) {
+      if (t.bytes) memcpy(t.dst, t.src, t.bytes);
+      return;
+    }
+    char** d = (char**)t.dst;
+    const int64_t* st = (const int64_t*)t.src;
+    for (uint64_t i = 0; i < t.bytes; ++i) d[i] = t.base + (t.len[i] > 0 ? st[i] - t.shift : 0);
+  }
   explicit CopyPool(unsigned helpers) {
     for (unsigned i = 0; i < helpers; ++i) ts_.emplace_back([this] { loop(); });
   }
@@ -167,23 +181,38 @@ class CopyPool {
   }
   CopyPool(const CopyPool&) = delete;
   CopyPool& operator=(const CopyPool&) = delete;
-  // run every copy of `tasks` (cut into <= 64 KB pieces) and return when all are done
+  // run every task (cut into <= 64 KB pieces; pointer tasks count 16 bytes a
+  // row) and return when all are done. (Smaller pieces for small batches
+  // measured slower: 8-16 KB pieces cost configs[4] 40 ms more per 10 M rows
+  // at capacity 1024, the claims and completions contending.)
   void run(const std::vector<Task>& tasks) {
     uint64_t total = 0;
-    for (const Task& t : tasks) total += t.bytes;
+    for (const Task& t : tasks) total += t.kind ? 16 * t.bytes : t.bytes;
     if (ts_.empty() || total < (96u << 10)) {
-      for (const Task& t : tasks)
-        if (t.bytes) memcpy(t.dst, t.src, t.bytes);
+      for (const Task& t : tasks) exec(t);
       return;
     }
     work_.clear();
-    constexpr uint64_t kPiece = 64u << 10;
-    for (const Task& t : tasks)
-      for (uint64_t o = 0; o < t.bytes; o += kPiece)
-        work_.push_back(Task{(char*)t.dst + o, (const char*)t.src + o, std::min(kPiece, t.bytes - o)});
+    constexpr uint64_t piece = 64u << 10;
+    for (const Task& t : tasks) {
+      if (t.kind == 0) {
+        for (uint64_t o = 0; o < t.bytes; o += piece)
+          work_.push_back(Task{(char*)t.dst + o, (const char*)t.src + o, std::min(piece, t.bytes - o)});
+      } else {
+        const uint64_t rows = std::max<uint64_t>(piece / 16, 1);
+        for (uint64_t o = 0; o < t.bytes; o += rows) {
+          Task q = t;
+          q.dst = (char**)t.dst + o;
+          q.src = (const int64_t*)t.src + o;
+          q.len = t.len + o;
+          q.bytes = std::min(rows, t.bytes - o);
+          work_.push_back(q);
+        }
+      }
+    }
     const uint64_t n = work_.size();
     if (n >= 0xffff) {  // (the claim word holds 16 bits of task count)
-      for (const Task& t : work_) memcpy(t.dst, t.src, t.bytes);
+      for (const Task& t : work_) exec(t);
       return;
     }
     const uint64_t g = ++gen_;
@@ -209,8 +238,7 @@ class CopyPool {
       const uint64_t cg = c >> 48, cn = (c >> 32) & 0xffff, k = c & 0xffffffffu;
       if (cg != (g & 0xffff) || k >= cn) return;
       if (!claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
-      const Task& t = work_[k];
-      memcpy(t.dst, t.src, t.bytes);
+      exec(work_[k]);
       done_.fetch_add(1, std::memory_order_acq_rel);
       c = claim_.load(std::memory_order_acquire);
     }
@@ -796,20 +824,19 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
           blob = std::make_shared<DataBuffer<char>>(r_.getMemoryPool(), v.blob_len);
           if (v.blob_len) memcpy(blob->data(), v.blob, v.blob_len);
         }
-        char* base = blob->data();
-        for (uint64_t i = 0; i < n; ++i) d[i] = base + (len[i] > 0 ? start[i] : 0);
+        if (n) copies_.push_back(CopyPool::Task{d, start, n, 1, len, blob->data(), 0});
       } else {
-        // direct: the byte span the batch covers
-        uint64_t lo = ~0ull, hi = 0;
-        for (uint64_t i = 0; i < n; ++i)
-          if (len[i] > 0) {
-            lo = std::min<uint64_t>(lo, (uint64_t)start[i]);
-            hi = std::max<uint64_t>(hi, (uint64_t)(start[i] + len[i]));
-          }
-        if (lo == ~0ull) lo = hi = 0;
+        // direct: the byte span the batch covers (non-empty values' starts
+        // ascend with the row: their first and last bound it)
+        uint64_t lo = 0, hi = 0, i0 = 0, i1 = n;
+        while (i0 < n && len[i0] <= 0) ++i0;
+        while (i1 > i0 && len[i1 - 1] <= 0) --i1;
+        if (i0 < i1) {
+          lo = (uint64_t)start[i0];
+          hi = (uint64_t)(start[i1 - 1] + len[i1 - 1]);
+        }
         copy(s.blob, v.blob, hi - lo, lo);
-        char* base = s.blob.data();
-        for (uint64_t i = 0; i < n; ++i) d[i] = base + (len[i] > 0 ? start[i] - (int64_t)lo : 0);
+        if (n) copies_.push_back(CopyPool::Task{d, start, n, 1, len, s.blob.data(), (int64_t)lo});
       }
       break;
     }

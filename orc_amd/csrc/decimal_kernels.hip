@@ -366,3 +366,11 @@ int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, in
 }
 
 }  // namespace orcg
+
+// A no-op launch that makes HIP load this file's code object (warm_modules).
+namespace orcg {
+namespace {
+__global__ void warm_decimal_kernel() {}
+}  // namespace
+void warm_decimal(hipStream_t s) { hipLaunchKernelGGL(warm_decimal_kernel, dim3(1), dim3(64), 0, s); }
+}  // namespace orcg

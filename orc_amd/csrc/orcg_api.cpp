@@ -157,7 +157,11 @@ constexpr size_t kHuge = size_t(2) << 20;
 
 void* pinned_alloc(size_t bytes) {
   if (bytes == 0) bytes = 1;
-  if (bytes >= (size_t(8) << 20)) {
+  static const int mode = [] {  // A/B: ORCG_PIN_MODE=1 always hipHostMalloc
+    const char* e = getenv("ORCG_PIN_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  if (mode == 0 && bytes >= (size_t(8) << 20)) {
     const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
     void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m != MAP_FAILED) {
@@ -320,6 +324,31 @@ int orcg_ctx_create(int device, orcg_ctx** out) {
     return ORCG_DEVICE_ERROR;
   }
   c->stream = c->own_stream;
+  // the process's first context on a device loads every kernel file's code
+  // object now (orcg_internal.hh warm_*)
+  static std::mutex warm_mu;
+  static std::vector<int> warmed;
+  static const bool warm = [] {
+    const char* e = getenv("ORCG_WARMUP");
+    return !e || atoi(e) != 0;
+  }();
+  if (warm) {
+    std::lock_guard<std::mutex> lk(warm_mu);
+    if (std::find(warmed.begin(), warmed.end(), device) == warmed.end()) {
+      warmed.push_back(device);
+      orcg::warm_rlev2_walk(c->stream);
+      orcg::warm_rlev2_tiled(c->stream);
+      orcg::warm_byterle(c->stream);
+      orcg::warm_columns(c->stream);
+      orcg::warm_rlev1(c->stream);
+      orcg::warm_decimal(c->stream);
+      if (hipStreamSynchronize(c->stream) != hipSuccess) {
+        (void)hipGetLastError();
+        orcg_ctx_destroy(c);
+        return ORCG_DEVICE_ERROR;
+      }
+    }
+  }
   *out = c;
   return ORCG_OK;
 }

@@ -75,6 +75,17 @@ struct Ctx {
 // Side context k of `base` (created on first use, settings copied from base);
 // nullptr if it cannot be created.
 Ctx* ctx_lane(Ctx* base, size_t k);
+// One no-op launch per kernel file on `s`: HIP loads a file's code object at
+// its first launch (tens of ms for all of them), so the first context of a
+// process pays it at creation instead of inside its first decode
+// (ORCG_WARMUP=0: lazily).
+void warm_rlev2_walk(hipStream_t s);
+void warm_rlev2_tiled(hipStream_t s);
+void warm_byterle(hipStream_t s);
+void warm_columns(hipStream_t s);
+void warm_rlev1(hipStream_t s);
+void warm_decimal(hipStream_t s);
+
 // Side streams the file reader may use (ORCG_LANES, default 4; 1 = none).
 unsigned side_lanes();
 

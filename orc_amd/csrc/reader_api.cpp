@@ -2963,6 +2963,9 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
   // the caller's kernel choice, snapshotted once: the worker never reads the
   // caller's context
   rr->own->rlev2_variant = r->own_ctx->rlev2_variant;
+  // its side lanes (streams, events, error records) now, not in the first
+  // stripe's decode
+  if (side_lanes() > 1) (void)ctx_lane(rr->own, side_lanes() - 1);
   const uint64_t ns = r->footer.stripes.size();
   rr->nstripes = ns;
   rr->current = ns;

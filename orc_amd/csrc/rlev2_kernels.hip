@@ -398,3 +398,11 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
 }
 
 }  // namespace orcg
+
+// A no-op launch that makes HIP load this file's code object (warm_modules).
+namespace orcg {
+namespace {
+__global__ void warm_rlev2_walk_kernel() {}
+}  // namespace
+void warm_rlev2_walk(hipStream_t s) { hipLaunchKernelGGL(warm_rlev2_walk_kernel, dim3(1), dim3(64), 0, s); }
+}  // namespace orcg
