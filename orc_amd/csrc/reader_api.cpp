@@ -1896,8 +1896,17 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& 
   parallel_for(rle.size(), [&](size_t q) {
     StreamBuf& sb = *rle[q];
     const uint8_t* p = hs.h + sb.host_off;
-    // byte / boolean RLE without row-index segments: 1 KB segments (one wave each: enough waves to fill the GPU)
-    if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, 1u << 10, 1024));
+    // byte / boolean RLE without row-index segments: 4 KB segments, one
+    // byterle_kernel window each (C5's child PRESENT streams: 45.7 -> 32.8 us
+    // a launch against 1 KB segments, whose workgroups each paid the
+    // window's fixed phase latencies for a quarter of the bytes;
+    // A/B: ORCG_BYTE_SEG_KB)
+    static const uint32_t byte_seg = [] {
+      const char* e = getenv("ORCG_BYTE_SEG_KB");
+      const int v = e ? atoi(e) : 4;
+      return (uint32_t)std::max(1, std::min(v, 64)) << 10;
+    }();
+    if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, byte_seg, byte_seg));
     else if (rle_kind[q] == 1)
       sb.plan.reset(make_v1_plan(p, sb.len, sb.len <= kV1SmallStream ? (1u << 10) : (16u << 10), 8192));
     else if (rle_kind[q] == 3) sb.plan.reset(make_plan(p, sb.len, 8u << 10, 4096));
