@@ -342,6 +342,19 @@ int orcg_ctx_create(int device, orcg_ctx** out) {
       orcg::warm_columns(c->stream);
       orcg::warm_rlev1(c->stream);
       orcg::warm_decimal(c->stream);
+      // and the copy paths: the process's first host <-> device copies cost
+      // ~10-100 ms of runtime setup (scripts/probes/pin_first_dma.py: a
+      // fresh pinned buffer copies at full rate afterwards)
+      void* h = nullptr;
+      void* dv = nullptr;
+      if (hipHostMalloc(&h, 4096, hipHostMallocDefault) == hipSuccess && hipMalloc(&dv, 4096) == hipSuccess) {
+        (void)hipMemcpyAsync(dv, h, 4096, hipMemcpyHostToDevice, c->stream);
+        (void)hipMemcpyAsync(h, dv, 4096, hipMemcpyDeviceToHost, c->stream);
+        (void)hipStreamSynchronize(c->stream);
+      }
+      (void)hipGetLastError();
+      if (dv) (void)hipFree(dv);
+      if (h) (void)hipHostFree(h);
       if (hipStreamSynchronize(c->stream) != hipSuccess) {
         (void)hipGetLastError();
         orcg_ctx_destroy(c);
