@@ -302,8 +302,9 @@ struct ColumnVectorBatch {
   uint32_t kind;  // orc::TypeKind
   uint64_t capacity;
   uint64_t numElements = 0;
-  DataBuffer<char> notNull;  // valid when hasNulls (ColumnReader::next leaves it alone otherwise)
+  DataBuffer<char> notNull;  // the rows' non-null flags (all 1 when !hasNulls)
   bool hasNulls = false;
+  bool notNullOnes_ = false;  // (adapter state: notNull holds only 1s)
   bool isEncoded = false;
   MemoryPool& memoryPool;
   const BatchClass cls;
@@ -762,8 +763,18 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
   b.numElements = n;
   if (n > b.capacity) b.capacity = n;  // children grow like the reference's resize()
   b.hasNulls = v.has_nulls != 0;
-  // notNull is meaningful only when hasNulls (ColumnReader::next)
-  if (b.hasNulls) copy(b.notNull, v.not_null, n, first);
+  // notNull: the decoded flags, or all 1s as the reference's PRESENT decode
+  // leaves them for a batch without nulls (ColumnReader::next,
+  // ColumnReader.cc:81-104), sized with a child's grown capacity; the 1s are
+  // rewritten only after a batch with nulls or a growth
+  if (b.hasNulls) {
+    copy(b.notNull, v.not_null, n, first);
+    b.notNullOnes_ = false;
+  } else if (!b.notNullOnes_ || b.notNull.size() < n) {
+    b.notNull.resize(std::max<uint64_t>(n, b.notNull.size()));
+    if (b.notNull.size()) memset(b.notNull.data(), 1, b.notNull.size());
+    b.notNullOnes_ = true;
+  }
   const std::vector<uint32_t>& subs = this->subs(id, v.kind);
   const char* nn = b.hasNulls ? (const char*)v.not_null + first : nullptr;
   switch (b.cls) {

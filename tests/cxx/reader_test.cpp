@@ -165,6 +165,27 @@ static std::string value(const ColumnVectorBatch& b, uint64_t i, const std::vect
   return "null";
 }
 
+// Every batch of the tree: notNull covers numElements rows and, when the
+// batch has no nulls, holds only 1s (the reference's ColumnReader::next
+// leaves the decoded all-ones PRESENT mask there).
+static bool not_null_ok(const ColumnVectorBatch& b) {
+  if (b.notNull.size() < b.numElements) return false;
+  if (!b.hasNulls)
+    for (uint64_t i = 0; i < b.numElements; ++i)
+      if (b.notNull[i] != 1) return false;
+  if (auto* lb = dynamic_cast<const ListVectorBatch*>(&b)) return not_null_ok(*lb->elements);
+  if (auto* mb = dynamic_cast<const MapVectorBatch*>(&b)) return not_null_ok(*mb->keys) && not_null_ok(*mb->elements);
+  if (auto* sb = dynamic_cast<const StructVectorBatch*>(&b)) {
+    for (const auto& f : sb->fields)
+      if (!not_null_ok(*f)) return false;
+  }
+  if (auto* ub = dynamic_cast<const UnionVectorBatch*>(&b)) {
+    for (const auto& c : ub->children)
+      if (!not_null_ok(*c)) return false;
+  }
+  return true;
+}
+
 static const RowReader* g_rows = nullptr;  // the row reader's selection (RowReader::getSelectedColumns)
 
 // the children a batch holds: a struct's selected fields, every other child
@@ -310,6 +331,10 @@ int main(int argc, char** argv) {
     while (rows->next(*batch)) {
       if (batch->numElements > cap) return 3;
       if (!ranged && rows->getRowNumber() != total) return 4;
+      if (!not_null_ok(*batch)) {
+        fprintf(stderr, "notNull: a batch without nulls has a 0 flag, or fewer flags than rows\n");
+        return 5;
+      }
       if (ranged && first) printf("#first %llu\n", (unsigned long long)rows->getRowNumber());
       first = false;
       for (uint64_t i = 0; i < batch->numElements; ++i) puts(row(reader, 0, *batch, i).c_str());

@@ -113,3 +113,57 @@ def test_hive11_overflow_becomes_null(tmp_path, with_present):
         while rr.next(batch):
             rows += [row["d"] for row in batch.to_pylist()]
         assert rows == want, cap
+
+
+def _hive11_multi_file(cols):
+    """struct<d0, d1, ...: decimal(0,0)> (type ids 0 .. k), one stripe, no row
+    index; cols = [(values, scales, present or None)], same row count."""
+    body, sf, n = b"", b"", None
+    for ci, (values, scales, present) in enumerate(cols, start=1):
+        sec, _ = orc_amd.encode_direct(np.asarray(scales, dtype=np.int64), True, aligned=True)
+        streams = []
+        if present is not None:
+            streams.append((0, ci, _bool_rle(present)))
+        streams += [(1, ci, b"".join(_zigzag_varint(v) for v in values)), (5, ci, sec.tobytes())]
+        for k, c, b in streams:
+            body += b
+            sf += field_bytes(1, field_varint(1, k) + field_varint(2, c) + field_varint(3, len(b)))
+        rows = len(present) if present is not None else len(values)
+        assert n is None or n == rows
+        n = rows
+    sf += field_bytes(2, field_varint(1, 0))  # root: DIRECT
+    sf += b"".join(field_bytes(2, field_varint(1, 2)) for _ in cols)  # decimals: DIRECT_V2
+    info = stripe_info(3, 0, len(body), len(sf), n)
+    types = [type_msg(12, list(range(1, len(cols) + 1)), ["d%d" % i for i in range(len(cols))])]
+    types += [type_msg(14) + field_varint(5, 0) + field_varint(6, 0) for _ in cols]
+    return orc_file(body + sf, [info], types, n)
+
+
+def test_hive11_overflow_sibling_columns(tmp_path):
+    """Sibling Hive 0.11 columns under the root struct decode on different
+    side streams (ORCG_LANES): each keeps its own overflow count and null
+    mask (a shared count word let one column read
+    another's)."""
+    rows = 11
+    vals_ok = [1, -2, 3, 4, 5, -6, 7, 8, 9, 10, 11]
+    vals_a = [12345, BIG, -7, 99, BIG * 5, 0, 15 * 10 ** 31, 42, 1, 2, 3]
+    vals_b = [5, 6, BIG, 8, 9, 10, 11]
+    pres_b = [1, 0, 1, 1, 0, 1, 1, 0, 1, 0, 1]
+    cols = [(vals_ok, [0] * rows, None), (vals_a, [2, 0, 0, 3, 1, 0, 0, 6, 1, 1, 1], None),
+            (vals_b, [1, 1, 1, 1, 1, 1, 1], pres_b), (list(reversed(vals_a)), [0] * rows, None)]
+    p = tmp_path / "h11_multi.orc"
+    p.write_bytes(_hive11_multi_file(cols))
+    want = [_expect(v, s, pr) for v, s, pr in cols]
+    r = orc_amd.Reader(str(p), orc_amd.default_context(0))
+    r.set_hive11_decimal(6, throw_on_overflow=False)
+    for _ in range(3):  # repeated stripe reads: each reuses the stripe's read-back block
+        b = r.read_stripe(0)
+        got = b.to_pylist()
+        for ci, w in enumerate(want):
+            assert [row["d%d" % ci] for row in got] == w, ci
+            c = b.columns[ci + 1]
+            if all(x is not None for x in w):
+                assert c.not_null is None or all(bool(x) for x in c.not_null[:rows]), ci
+            else:
+                assert c.not_null is not None, ci
+                assert [bool(x) for x in c.not_null[:rows]] == [x is not None for x in w], ci
