@@ -1214,6 +1214,56 @@ __device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT
     uint16_t* ta = s_nxt;
     uint16_t* tb = s_nxt + kSlab;
     put8(ta);
+#ifndef ORCG_DOUBLING_CHAIN
+    // (2) the chain by hops, O(slab) work in three barriers: ta = each
+    // position's block exit; tb = its 64-byte super-block exit (<= 7 hops
+    // over ta, every thread for its 8 positions); one lane hops the <= 32
+    // super-blocks from position 0 and records each one's first chain
+    // position; every thread hops from its super-block's entry to its own
+    // block (<= 7 hops). The pointer doubling below (ORCG_DOUBLING_CHAIN)
+    // took 8 levels of marks and gathers over the whole slab.
+    constexpr uint32_t kSup = 8u * kBlk;
+    __syncthreads();
+    {
+      const uint32_t send = (lo / kSup + 1u) * kSup;
+      uint32_t q[kBlk];
+  #pragma unroll
+      for (int e = 0; e < (int)kBlk; ++e) q[e] = na[e];
+  #pragma unroll
+      for (int h = 0; h < 7; ++h) {
+  #pragma unroll
+        for (int e = 0; e < (int)kBlk; ++e) {
+          const bool in = q[e] != kSink && q[e] < send;
+          const uint32_t v = ta[in ? q[e] : lo + (uint32_t)e];
+          q[e] = in ? v : q[e];
+        }
+      }
+      typedef uint32_t u4h __attribute__((ext_vector_type(4)));
+      u4h w;
+      w.x = q[0] | q[1] << 16;
+      w.y = q[2] | q[3] << 16;
+      w.z = q[4] | q[5] << 16;
+      w.w = q[6] | q[7] << 16;
+      *(u4h*)(tb + lo) = w;
+    }
+    if (tid < (int)(kSlab / kSup)) s_mark[tid] = kSink;  // the super-blocks' chain entries
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t p = 0;
+      while (p != kSink && p < lim) {
+        s_mark[p / kSup] = p;
+        p = tb[p];
+      }
+    }
+    __syncthreads();
+    {
+      uint32_t p = s_mark[lo / kSup];
+      for (int h = 0; h < 7 && p != kSink && p < lo; ++h) p = ta[p];
+      has = p != kSink && p >= lo && p < hi && p < lim;
+      eb = has ? p - lo : 0u;
+    }
+    static_assert(kSlab / kSup <= kSlab / 32, "super-block entries fit the marks");
+#else
     if (tid < (int)(kSlab / 32)) s_mark[tid] = tid == 0;  // position 0 starts the chain
     __syncthreads();
   #pragma unroll 1
@@ -1249,6 +1299,7 @@ __device__ __forceinline__ DenseResult dense2_discover(const uint32_t* win, OffT
     const uint32_t mb = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
     has = mb != 0;
     eb = has ? (uint32_t)__builtin_ctz(mb) : 0u;
+#endif
   }
   PROF_MARK(4);
   // (3) the block's entry, its runs (a forward pass over the DP registers),
