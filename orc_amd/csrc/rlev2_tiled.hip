@@ -2178,35 +2178,20 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   };
 
   if constexpr (kDefer == 2) {
-    // the drain: workgroup w takes the contiguous share [w C, (w + 1) C) of
-    // the launch's segments, finds the ones the serial launch stamped with
-    // this pair's sequence number (one stamp load per thread, a ballot per
-    // wave: an empty share costs one load round) and decodes the rest of
-    // each (no counters)
-    __shared__ unsigned long long s_flags[kWaves];
+    // the drain: one workgroup per launch-wide segment; a segment the serial
+    // launch stamped with this pair's sequence number is decoded from its
+    // queued byte offset / value index, any other exits after one load (the
+    // hardware hands out the queued segments as workgroups free up: the
+    // earlier persistent grid of 6 workgroups per CU, each a static share,
+    // ran 19 % slower on all-short-run streams)
     // nothing queued by the serial launch (long-run streams): one load, exit
     if (uni64(__hip_atomic_load(&defer_q[3 * p_nsegs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
         (unsigned long long)defer_par)
       return;
-    const uint64_t per = (p_nsegs + gridDim.x - 1) / gridDim.x;
-    const uint64_t g0 = (uint64_t)blockIdx.x * per;
-    const uint64_t g1 = min(g0 + per, p_nsegs);
-    for (uint64_t b = g0; b < g1; b += kThreads) {
-      const uint64_t g = b + (uint64_t)tid;
-      const bool mine = g < g1 && defer_q[3 * g] == (unsigned long long)defer_par;
-      const unsigned long long m = __ballot(mine);
-      if (lane == 0) s_flags[wave] = m;
-      __syncthreads();
-      for (int w = 0; w < kWaves; ++w) {
-        for (unsigned long long f = uni64(s_flags[w]); f; f &= f - 1) {
-          const uint64_t q = b + (uint64_t)(w * kWave + __builtin_ctzll(f));
-          run_segment(q, true, uni64(defer_q[3 * q + 1]), uni64(defer_q[3 * q + 2]));
-          place(q);
-          __syncthreads();  // LDS is reused by the next segment
-        }
-      }
-      __syncthreads();  // s_flags is rewritten by the next round
-    }
+    const uint64_t q = blockIdx.x;
+    if (q >= p_nsegs || uni64(defer_q[3 * q]) != (unsigned long long)defer_par) return;
+    run_segment(q, true, uni64(defer_q[3 * q + 1]), uni64(defer_q[3 * q + 2]));
+    place(q);
   } else {
     // (one call site per instance: a second one makes the compiler outline
     // run_segment into a call with a ~700-byte stack frame)
@@ -2308,16 +2293,12 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
   const int sg = is_signed ? 1 : 0;
   unsigned long long* dq = nullptr;
   uint32_t dpar = 0;
-  // the queue consumer is a persistent grid of exactly the resident
-  // workgroups (6 per CU for the 8.5 KB dense instance): entries are dealt
-  // out statically, so a workgroup that starts late would finish late
   if (ctx->num_cus == 0) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
       cus = 256;
     ctx->num_cus = cus;
   }
-  const unsigned drain = (unsigned)std::min<uint64_t>(nsegs, 6ull * (uint64_t)ctx->num_cus);
 
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
   hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
@@ -2375,7 +2356,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     dpar = (uint32_t)(ctx->defer_seq++ % 0xffffffffull) + 1u; /* never 0 */         \
     ORCG_KX(O, WKB, false, MWV, 0, 1, (unsigned)nsegs);                              \
     debug_defer(ctx, dq, nsegs, dpar);                                                \
-    ORCG_KX(DO, 8, false, 6, 2, 2, drain);                                           \
+    ORCG_KX(DO, 8, false, 6, 2, 2, (unsigned)nsegs);                                 \
   } while (0)
 
   const unsigned grid_s = (unsigned)nsegs;
