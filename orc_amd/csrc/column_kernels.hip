@@ -366,6 +366,100 @@ __global__ __launch_bounds__(kThreads) void tile_scan_kernel(const int64_t* __re
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = (int64_t)tile_off[gridDim.x];
 }
 
+// Single-pass exclusive scan (decoupled look-back): workgroup tickets in
+// dispatch order (an atomic on status[ntiles]); a tile's 4,096 values are
+// loaded coalesced into LDS (row k*256 + tid), scanned 16 consecutive per
+// thread, and stored back coalesced. Each tile publishes its aggregate
+// (kLbA) as soon as it has it and its inclusive prefix (kLbP) once known; one
+// wave looks back over 64 predecessors at a time, waiting on any still
+// unpublished, summing back to the nearest inclusive prefix. status[] (ntiles
+// + 1 words) is zeroed before the launch. The three-launch scan above read
+// 16 consecutive values per lane (one 128-byte stride per load instruction):
+// 18-28 us per kernel for configs[4]'s 2.6 M list lengths.
+constexpr uint64_t kLbA = 1ull << 62, kLbP = 2ull << 62, kLbVal = (1ull << 62) - 1;
+
+__global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const int64_t* __restrict__ in, uint64_t n,
+                                                                 int64_t* __restrict__ out,
+                                                                 unsigned long long* __restrict__ status,
+                                                                 uint32_t ntiles) {
+  __shared__ uint64_t s_v[kScanTile + kScanTile / 16];  // one pad word per thread's 16 (bank spread)
+  __shared__ uint64_t s_wsum[kThreads / kWave];
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_excl;
+  const int tid = (int)threadIdx.x, lane = tid % kWave, wv = tid / kWave;
+  if (tid == 0) s_tile = atomicAdd((unsigned int*)&status[ntiles], 1u);
+  __syncthreads();
+  const uint32_t t = s_tile;
+  const uint64_t base = (uint64_t)t * kScanTile;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t i = base + (uint64_t)k * kThreads + tid;
+    const uint32_t e = (uint32_t)(k * kThreads + tid);
+    s_v[e + (e >> 4)] = i < n ? (uint64_t)in[i] : 0ull;
+  }
+  __syncthreads();
+  uint64_t v[16], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    v[k] = s_v[tid * 17 + k];
+    sum += v[k];
+  }
+  const uint64_t inc = wave_inclusive_scan(sum);
+  if (lane == kWave - 1) s_wsum[wv] = inc;
+  __syncthreads();
+  uint64_t before = inc - sum, agg = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / kWave; ++w) {
+    const uint64_t c = s_wsum[w];
+    before += w < wv ? c : 0ull;
+    agg += c;
+  }
+  if (wv == 0) {
+    uint64_t excl = 0;
+    if (t == 0) {
+      if (lane == 0) __hip_atomic_store(&status[0], kLbP | (agg & kLbVal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&status[t], kLbA | (agg & kLbVal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int64_t j = (int64_t)t - 1;; j -= kWave) {
+        const int64_t k = j - lane;
+        uint64_t st = kLbP;  // before tile 0: an inclusive prefix of 0
+        if (k >= 0) st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__ballot(k >= 0 && (st >> 62) == 0) != 0) {
+          if (k >= 0 && (st >> 62) == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        const uint64_t pm = __ballot((st >> 62) == 2);
+        const int first = pm ? __builtin_ctzll(pm) : kWave;  // the nearest inclusive prefix
+        uint64_t c = lane <= first ? (st & kLbVal) : 0ull;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+        excl += c;
+        if (pm) break;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[t], kLbP | ((excl + agg) & kLbVal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  uint64_t run = s_excl + before;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    s_v[tid * 17 + k] = run;
+    run += v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint64_t i = base + (uint64_t)k * kThreads + tid;
+    const uint32_t e = (uint32_t)(k * kThreads + tid);
+    if (i < n) out[i] = (int64_t)s_v[e + (e >> 4)];
+  }
+  if (t == ntiles - 1 && tid == kThreads - 1) out[n] = (int64_t)(s_excl + agg);
+}
+
 // Element conversions into the reference's batch types (LongVectorBatch /
 // DoubleVectorBatch): tinyint sign-extension (ByteColumnReader, c++/src/
 // ColumnReader.cc:188-223), boolean 0/1 (BooleanColumnReader :131-186),
@@ -598,6 +692,17 @@ int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_
   }
   const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
   if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many values");
+  static const bool three = getenv("ORCG_SCAN3") != nullptr;  // A/B: the three-launch scan
+  if (!three) {
+    void* d_status;
+    int rc = scratch(ctx, 7, (tiles + 1) * sizeof(uint64_t), &d_status);
+    if (rc) return rc;
+    rc = hip_check(ctx, hipMemsetAsync(d_status, 0, (tiles + 1) * sizeof(uint64_t), ctx->stream), "scan status reset");
+    if (rc) return rc;
+    hipLaunchKernelGGL(scan_lookback_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n, d_out,
+                       (unsigned long long*)d_status, (uint32_t)tiles);
+    return hip_check(ctx, hipGetLastError(), "scan launch");
+  }
   void* d_sums;
   int rc = scratch(ctx, 7, (2 * tiles + 1) * sizeof(uint64_t), &d_sums);
   if (rc) return rc;

@@ -734,3 +734,11 @@ const char* orcg_rle_decoder_last_error(const orcg_rle_decoder* d) {
 }
 
 }  // extern "C"
+
+// Test hook (tests/test_gpu_scan.py): the reader's exclusive scan of int64
+// values, d_out[0..n] (n + 1 entries), on the context's stream.
+extern "C" int orcg_debug_exclusive_scan(orcg_ctx* c, const int64_t* d_in, uint64_t n, int64_t* d_out) {
+  if (!c || (n && !d_in) || !d_out) return ORCG_INVALID_ARGUMENT;
+  hipSetDevice(c->device);
+  return orcg::launch_exclusive_scan(c, d_in, n, d_out);
+}
