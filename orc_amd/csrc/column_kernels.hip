@@ -40,6 +40,62 @@ __device__ __forceinline__ u4 load16(const uint8_t* nn, uint64_t row0, uint64_t 
   return v;
 }
 
+// ---- decoupled look-back (single-pass scans; no reset launch) ----------
+// A tile's status word: epoch << 48 | flag << 46 | value (46 bits); flag 1 =
+// the tile's aggregate, 2 = its inclusive prefix. A word of another epoch is
+// unpublished, so the context's buffer is never cleared between launches
+// (lb_status hands out a new 16-bit epoch per launch). The word before the
+// status words counts tickets: tiles take them in the order they start (so a
+// tile only waits on tiles already running), and the tile that takes the
+// launch's last ticket sets the counter back to 0 for the next launch on the
+// stream (a compare-and-swap ticket on an epoch-tagged word instead cost
+// 40x: thousands of workgroups retrying on one address).
+constexpr uint64_t kLbMask = (1ull << 46) - 1;
+
+__device__ __forceinline__ uint32_t lb_ticket(unsigned long long* status, uint32_t ntiles) {
+  unsigned int* ctr = (unsigned int*)(status - 1);
+  const uint32_t t = atomicAdd(ctr, 1u);
+  if (t == ntiles - 1) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return t;
+}
+
+__device__ __forceinline__ void lb_publish(unsigned long long* status, uint32_t t, uint32_t flag, uint64_t v,
+                                           uint32_t epoch) {
+  __hip_atomic_store(&status[t],
+                     ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46) | (v & kLbMask),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave of tile t > 0 (after it published its aggregate): the sum over
+// tiles [0, t), 64 predecessors a round back to the nearest inclusive prefix.
+__device__ uint64_t lb_lookback(unsigned long long* status, uint32_t t, uint32_t epoch, int lane) {
+  uint64_t excl = 0;
+  for (int64_t j = (int64_t)t - 1;; j -= kWave) {
+    const int64_t k = j - lane;
+    unsigned long long st = 0;
+    uint32_t fl = 2;  // before tile 0: an inclusive prefix of 0
+    if (k >= 0) {
+      st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      fl = (uint32_t)(st >> 48) == epoch ? (uint32_t)((st >> 46) & 3u) : 0u;
+    }
+    while (__ballot(fl == 0) != 0) {
+      if (fl == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fl = (uint32_t)(st >> 48) == epoch ? (uint32_t)((st >> 46) & 3u) : 0u;
+      }
+    }
+    const uint64_t pm = __ballot(fl == 2);
+    const int first = pm ? __builtin_ctzll(pm) : kWave;
+    uint64_t c = (k >= 0 && lane <= first) ? (uint64_t)(st & kLbMask) : 0ull;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+    excl += c;
+    if (pm) break;
+  }
+  return excl;
+}
+
 __global__ __launch_bounds__(kThreads) void tile_count_kernel(const uint8_t* __restrict__ nn, uint64_t n,
                                                                uint32_t* __restrict__ counts) {
   __shared__ uint32_t red[kThreads / kWave];
@@ -373,21 +429,19 @@ __global__ __launch_bounds__(kThreads) void tile_scan_kernel(const int64_t* __re
 // (kLbA) as soon as it has it and its inclusive prefix (kLbP) once known; one
 // wave looks back over 64 predecessors at a time, waiting on any still
 // unpublished, summing back to the nearest inclusive prefix. status[] (ntiles
-// + 1 words) is zeroed before the launch. The three-launch scan above read
+// + 1 words, epoch-tagged) need no reset. The three-launch scan above read
 // 16 consecutive values per lane (one 128-byte stride per load instruction):
 // 18-28 us per kernel for configs[4]'s 2.6 M list lengths.
-constexpr uint64_t kLbA = 1ull << 62, kLbP = 2ull << 62, kLbVal = (1ull << 62) - 1;
-
 __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const int64_t* __restrict__ in, uint64_t n,
                                                                  int64_t* __restrict__ out,
                                                                  unsigned long long* __restrict__ status,
-                                                                 uint32_t ntiles) {
+                                                                 uint32_t ntiles, uint32_t epoch) {
   __shared__ uint64_t s_v[kScanTile + kScanTile / 16];  // one pad word per thread's 16 (bank spread)
   __shared__ uint64_t s_wsum[kThreads / kWave];
   __shared__ uint32_t s_tile;
   __shared__ uint64_t s_excl;
   const int tid = (int)threadIdx.x, lane = tid % kWave, wv = tid / kWave;
-  if (tid == 0) s_tile = atomicAdd((unsigned int*)&status[ntiles], 1u);
+  if (tid == 0) s_tile = lb_ticket(status, ntiles);
   __syncthreads();
   const uint32_t t = s_tile;
   const uint64_t base = (uint64_t)t * kScanTile;
@@ -417,29 +471,11 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const int64_t* 
   if (wv == 0) {
     uint64_t excl = 0;
     if (t == 0) {
-      if (lane == 0) __hip_atomic_store(&status[0], kLbP | (agg & kLbVal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) lb_publish(status, 0, 2, agg, epoch);
     } else {
-      if (lane == 0) __hip_atomic_store(&status[t], kLbA | (agg & kLbVal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (int64_t j = (int64_t)t - 1;; j -= kWave) {
-        const int64_t k = j - lane;
-        uint64_t st = kLbP;  // before tile 0: an inclusive prefix of 0
-        if (k >= 0) st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (__ballot(k >= 0 && (st >> 62) == 0) != 0) {
-          if (k >= 0 && (st >> 62) == 0) {
-            __builtin_amdgcn_s_sleep(1);
-            st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-        const uint64_t pm = __ballot((st >> 62) == 2);
-        const int first = pm ? __builtin_ctzll(pm) : kWave;  // the nearest inclusive prefix
-        uint64_t c = lane <= first ? (st & kLbVal) : 0ull;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
-        excl += c;
-        if (pm) break;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&status[t], kLbP | ((excl + agg) & kLbVal), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) lb_publish(status, t, 1, agg, epoch);
+      excl = lb_lookback(status, t, epoch, lane);
+      if (lane == 0) lb_publish(status, t, 2, excl + agg, epoch);
     }
     if (lane == 0) s_excl = excl;
   }
@@ -536,6 +572,68 @@ __global__ void rg_segtab_kernel(const int64_t* __restrict__ trip, const int64_t
   seg[2 * g + 1] = (uint64_t)v;
 }
 
+// rg_count + scan + rg_segtab in one launch: tile t (a ticket) counts row
+// group t's set mask bytes, looks back for the set rows before it (decoupled
+// look-back over the row groups) and writes prefix[t] and segment t; the
+// last row group also writes prefix[G]. (Three dependent launches per
+// masked row-index stream before: ~16 us of a nullable column's chain.)
+__global__ __launch_bounds__(kThreads) void rg_prefix_segtab_kernel(const uint8_t* __restrict__ mask, uint64_t n,
+                                                                    const int64_t* __restrict__ rows, uint64_t G,
+                                                                    const int64_t* __restrict__ trip, int boolean,
+                                                                    int64_t* __restrict__ prefix,
+                                                                    uint64_t* __restrict__ seg,
+                                                                    unsigned long long* __restrict__ status,
+                                                                    uint32_t epoch) {
+  __shared__ uint32_t red[kThreads / kWave];
+  __shared__ uint32_t s_t;
+  const int tid = (int)threadIdx.x, lane = tid % kWave, wv = tid / kWave;
+  if (tid == 0) s_t = lb_ticket(status, (uint32_t)G);
+  __syncthreads();
+  const uint32_t g = s_t;
+  uint64_t a = (uint64_t)rows[g], b = g + 1 < G ? (uint64_t)rows[g + 1] : n;
+  if (a > n) a = n;
+  if (b > n) b = n;
+  uint32_t c = 0;
+  if (b > a) {
+    const uintptr_t pa = (uintptr_t)(mask + a), pb = (uintptr_t)(mask + b);
+    const uintptr_t ma = (pa + 15) & ~(uintptr_t)15, mb = pb & ~(uintptr_t)15;
+    if (ma < mb) {
+      const u4* v = (const u4*)ma;
+      const uint64_t nv = (uint64_t)(mb - ma) / 16;
+      for (uint64_t k = (uint64_t)tid; k < nv; k += kThreads) c += nn_bytes_count(v[k]);
+      for (uintptr_t q = pa + tid; q < ma; q += kThreads) c += *(const uint8_t*)q != 0;
+      for (uintptr_t q = mb + tid; q < pb; q += kThreads) c += *(const uint8_t*)q != 0;
+    } else {
+      for (uint64_t r = a + tid; r < b; r += kThreads) c += mask[r] != 0;
+    }
+  }
+  for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor((int)c, m);
+  if (lane == 0) red[wv] = c;
+  __syncthreads();
+  if (wv == 0) {
+    uint64_t agg = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / kWave; ++w) agg += red[w];
+    uint64_t excl = 0;
+    if (g == 0) {
+      if (lane == 0) lb_publish(status, 0, 2, agg, epoch);
+    } else {
+      if (lane == 0) lb_publish(status, g, 1, agg, epoch);
+      excl = lb_lookback(status, g, epoch, lane);
+      if (lane == 0) lb_publish(status, g, 2, excl + agg, epoch);
+    }
+    if (lane == 0) {
+      prefix[g] = (int64_t)excl;
+      if (g + 1 == G) prefix[G] = (int64_t)(excl + agg);
+      const int64_t off = trip[3 * g], skip = trip[3 * g + 1], bits = trip[3 * g + 2];
+      int64_t v = boolean ? ((int64_t)excl - bits) / 8 - skip : (int64_t)excl - skip;
+      if (v < 0) v = 0;  // a corrupt index: the decode reports the segment mismatch
+      seg[2 * g] = (uint64_t)off;
+      seg[2 * g + 1] = (uint64_t)v;
+    }
+  }
+}
+
 // child row group starts of a list / map column: offsets[parent rows[g]]
 __global__ void rg_child_rows_kernel(const int64_t* __restrict__ offsets, const int64_t* __restrict__ rows,
                                      uint64_t G, int64_t* __restrict__ out) {
@@ -580,6 +678,35 @@ __global__ void union_offsets_kernel(const uint8_t* __restrict__ tags, uint64_t 
 }
 
 }  // namespace
+
+// The context's look-back status words for `words` entries and a fresh
+// epoch (a new buffer is zeroed; epochs wrap at 16 bits with one clear).
+static int lb_status(Ctx* ctx, uint64_t words, unsigned long long** out, uint32_t* epoch) {
+  words += 1;  // the ticket counter
+  if (ctx->lb_cap < words) {
+    if (ctx->d_lb) {
+      int rc = hip_check(ctx, hipStreamSynchronize(ctx->stream), "look-back status sync");
+      if (rc) return rc;
+      (void)hipFree(ctx->d_lb);
+      ctx->d_lb = nullptr;
+      ctx->lb_cap = 0;
+    }
+    const uint64_t cap = std::max<uint64_t>(words + words / 4, 1u << 14);
+    int rc = hip_check(ctx, hipMalloc(&ctx->d_lb, cap * 8), "hipMalloc look-back status");
+    if (!rc) rc = hip_check(ctx, hipMemsetAsync(ctx->d_lb, 0, cap * 8, ctx->stream), "look-back status clear");
+    if (rc) return rc;
+    ctx->lb_cap = cap;
+    ctx->lb_epoch = 0;
+  }
+  if (++ctx->lb_epoch > 0xffffu) {
+    const int rc = hip_check(ctx, hipMemsetAsync(ctx->d_lb, 0, ctx->lb_cap * 8, ctx->stream), "look-back status clear");
+    if (rc) return rc;
+    ctx->lb_epoch = 1;
+  }
+  *out = (unsigned long long*)ctx->d_lb + 1;  // word 0: the ticket counter
+  *epoch = ctx->lb_epoch;
+  return ORCG_OK;
+}
 
 // 16-byte elements (Decimal128 values, orc::Int128 layout [hi, lo])
 struct alignas(16) Pair128 {
@@ -694,13 +821,12 @@ int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_
   if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many values");
   static const bool three = getenv("ORCG_SCAN3") != nullptr;  // A/B: the three-launch scan
   if (!three) {
-    void* d_status;
-    int rc = scratch(ctx, 7, (tiles + 1) * sizeof(uint64_t), &d_status);
-    if (rc) return rc;
-    rc = hip_check(ctx, hipMemsetAsync(d_status, 0, (tiles + 1) * sizeof(uint64_t), ctx->stream), "scan status reset");
+    unsigned long long* d_status;
+    uint32_t epoch;
+    const int rc = lb_status(ctx, tiles + 1, &d_status, &epoch);
     if (rc) return rc;
     hipLaunchKernelGGL(scan_lookback_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n, d_out,
-                       (unsigned long long*)d_status, (uint32_t)tiles);
+                       d_status, (uint32_t)tiles, epoch);
     return hip_check(ctx, hipGetLastError(), "scan launch");
   }
   void* d_sums;
@@ -802,6 +928,19 @@ int launch_rg_segtab(Ctx* ctx, const int64_t* d_trip, const int64_t* d_prefix, u
   hipLaunchKernelGGL(rg_segtab_kernel, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, ctx->stream, d_trip,
                      d_prefix, G, boolean ? 1 : 0, d_seg);
   return hip_check(ctx, hipGetLastError(), "rg_segtab_kernel launch");
+}
+
+int launch_rg_prefix_segtab(Ctx* ctx, const uint8_t* d_mask, uint64_t n, const int64_t* d_rows, uint64_t G,
+                            const int64_t* d_trip, bool boolean, int64_t* d_prefix, uint64_t* d_seg) {
+  if (G == 0) return ORCG_OK;
+  if (G > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many row groups");
+  unsigned long long* d_status;
+  uint32_t epoch;
+  const int rc = lb_status(ctx, G + 1, &d_status, &epoch);
+  if (rc) return rc;
+  hipLaunchKernelGGL(rg_prefix_segtab_kernel, dim3((unsigned)G), dim3(kThreads), 0, ctx->stream, d_mask, n, d_rows, G,
+                     d_trip, boolean ? 1 : 0, d_prefix, d_seg, d_status, epoch);
+  return hip_check(ctx, hipGetLastError(), "rg_prefix_segtab_kernel launch");
 }
 
 int launch_rg_child_rows(Ctx* ctx, const int64_t* d_offsets, const int64_t* d_rows, uint64_t G, int64_t* d_out) {

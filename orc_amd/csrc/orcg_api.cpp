@@ -383,6 +383,7 @@ void orcg_ctx_destroy(orcg_ctx* c) {
   if (c->h_pinned) hipHostFree(c->h_pinned);
   if (c->d_err) hipFree(c->d_err);
   if (c->d_defer) hipFree(c->d_defer);
+  if (c->d_lb) hipFree(c->d_lb);
   if (c->d_jobs) hipFree(c->d_jobs);
   if (c->h_jobs) hipHostFree(c->h_jobs);
   if (c->own_stream) hipStreamDestroy(c->own_stream);

@@ -53,6 +53,11 @@ struct Ctx {
   uint64_t defer_cap = 0;
   uint64_t defer_seq = 0;  // serial + drain launch pairs so far (their entries' stamps)
   int num_cus = 0;         // compute units of `device` (0 = not queried yet)
+  // decoupled look-back status words (column_kernels.hip lb_status): one
+  // buffer per context (its launches are ordered), a 16-bit epoch per launch
+  void* d_lb = nullptr;
+  uint64_t lb_cap = 0;
+  uint32_t lb_epoch = 0;
   // job tables of multi-stream launches: a pinned host ring and its device
   // mirror, in bytes (stage_table)
   void* h_jobs = nullptr;
@@ -268,6 +273,10 @@ int launch_rg_prefix(Ctx* ctx, const uint8_t* d_mask, uint64_t n, const int64_t*
 int launch_rg_segtab(Ctx* ctx, const int64_t* d_trip, const int64_t* d_prefix, uint64_t G, bool boolean,
                      uint64_t* d_seg);
 int launch_rg_child_rows(Ctx* ctx, const int64_t* d_offsets, const int64_t* d_rows, uint64_t G, int64_t* d_out);
+// rg_prefix + rg_segtab in one launch (decoupled look-back over the row
+// groups' counts): d_prefix (G + 1 entries) and the segment table.
+int launch_rg_prefix_segtab(Ctx* ctx, const uint8_t* d_mask, uint64_t n, const int64_t* d_rows, uint64_t G,
+                            const int64_t* d_trip, bool boolean, int64_t* d_prefix, uint64_t* d_seg);
 
 // UNION tags (UnionColumnReader): flags[j] = tags[j] == k; the first tag >=
 // nchildren as (index << 8 | tag), ~0 when none; offsets[j] = scan_k[j] for

@@ -706,6 +706,20 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
   const uint8_t* mask = slot == kSlotPresent ? cur_in_nn : cur_row_nn;
   const int64_t* prefix = cur_rows;
   int rc;
+  static const bool three = getenv("ORCG_SCAN3") != nullptr;  // A/B: count, scan and segtab launches
+  if (mask && !three) {
+    // the row groups' set-row prefix and the segment table in one launch
+    ORCG_ALLOC(int64_t, pre, G + 1);
+    ORCG_ALLOC(uint64_t, seg, 2 * G);
+    if ((rc = launch_rg_prefix_segtab(ctx, mask, cur_n, cur_rows, G, (const int64_t*)(D->d_stage + sb.rg_off), boolean,
+                                      pre, seg)))
+      return fail_ctx(rc);
+    seg_prefix = pre;
+    seg_mask = mask;
+    *d_seg = seg;
+    *nseg = G;
+    return ORCG_OK;
+  }
   if (mask) {
     ORCG_ALLOC(int64_t, counts, G);
     ORCG_ALLOC(int64_t, pre, G + 1);

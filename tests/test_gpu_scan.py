@@ -33,3 +33,27 @@ def test_exclusive_scan_matches_numpy(n):
         ctx.synchronize()
         want = np.concatenate([[0], np.cumsum(x)]).astype(np.int64)
         np.testing.assert_array_equal(d_out.cpu().numpy(), want)
+
+
+def test_exclusive_scan_epoch_wrap():
+    """The look-back status words carry a 16-bit launch epoch (no clearing
+    launch); past 65,535 launches on one context the buffer is cleared once
+    and the epochs restart: results stay exact across the wrap."""
+    import torch
+
+    L = orc_amd._lib.load()
+    f = L.orcg_debug_exclusive_scan
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+    ctx = orc_amd.Context(0)
+    n = 3 * 4096 + 5
+    x = np.arange(n, dtype=np.int64) % 7
+    d_in = torch.from_numpy(x).cuda()
+    d_out = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    want = np.concatenate([[0], np.cumsum(x)]).astype(np.int64)
+    for i in range(66_000):
+        rc = f(ctx.handle, d_in.data_ptr(), n, d_out.data_ptr())
+        assert rc == 0, ctx.last_error
+        if i in (0, 65_533, 65_534, 65_535, 65_999):
+            ctx.synchronize()
+            np.testing.assert_array_equal(d_out.cpu().numpy(), want)
