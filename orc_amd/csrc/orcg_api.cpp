@@ -355,6 +355,22 @@ int orcg_ctx_create(int device, orcg_ctx** out) {
       (void)hipGetLastError();
       if (dv) (void)hipFree(dv);
       if (h) (void)hipHostFree(h);
+      // large copies take the DMA engines (small ones a blit kernel): one
+      // each way from registered pinned memory (ORCG_WARMUP_MB, default 16)
+      static const size_t big = [] {
+        const char* e = getenv("ORCG_WARMUP_MB");
+        return (size_t)(e ? std::max(0, atoi(e)) : 16) << 20;
+      }();
+      void* hb = big ? pinned_alloc(big) : nullptr;
+      void* db = nullptr;
+      if (hb && hipMalloc(&db, big) == hipSuccess) {
+        (void)hipMemcpyAsync(db, hb, big, hipMemcpyHostToDevice, c->stream);
+        (void)hipMemcpyAsync(hb, db, big, hipMemcpyDeviceToHost, c->stream);
+        (void)hipStreamSynchronize(c->stream);
+      }
+      (void)hipGetLastError();
+      if (db) (void)hipFree(db);
+      if (hb) pinned_free(hb);
       if (hipStreamSynchronize(c->stream) != hipSuccess) {
         (void)hipGetLastError();
         orcg_ctx_destroy(c);
