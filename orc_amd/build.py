@@ -17,7 +17,7 @@ OUT = os.path.join(HERE, "liborcgpu_prof.so" if PROF else ("liborcgpu_ab.so" if 
 OBJ = os.path.join(HERE, "build_prof" if PROF else ("build_ab" if AB else "build"))
 ARCH = os.environ.get("ORCG_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "decimal_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "decimal_api.cpp", "encoder.cpp", "java_face.cpp"]
+SOURCES = ["rlev2_kernels.hip", "rlev2_tiled.hip", "rlev2_expand.hip", "byterle_kernels.hip", "column_kernels.hip", "rlev1_kernels.hip", "decimal_kernels.hip", "orcg_api.cpp", "rlev1_api.cpp", "orc_file.cpp", "reader_api.cpp", "byterle_api.cpp", "decimal_api.cpp", "encoder.cpp", "java_face.cpp"]
 if PROF or AB:
     SOURCES.append("probe_kernels.hip")
 HEADERS = ["orcg_internal.hh", "rlev2_device.hh", "orc_file.hh", os.path.join("..", "..", "include", "orcg.h"),

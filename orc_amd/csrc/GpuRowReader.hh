@@ -845,6 +845,10 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
         if (i0 < i1) {
           lo = (uint64_t)start[i0];
           hi = (uint64_t)(start[i1 - 1] + len[i1 - 1]);
+          // the decode rejects negative lengths and short blobs; never build
+          // pointers outside the stripe's bytes whatever the views say
+          if (start[i0] < 0 || hi < lo || hi > v.blob_len)
+            throw ParseError("failed to read in StringDirectColumnReader.next");
         }
         copy(s.blob, v.blob, hi - lo, lo);
         if (n) copies_.push_back(CopyPool::Task{d, start, n, 1, len, s.blob.data(), (int64_t)lo});

@@ -41,16 +41,24 @@ __device__ __forceinline__ u4 load16(const uint8_t* nn, uint64_t row0, uint64_t 
 }
 
 // ---- decoupled look-back (single-pass scans; no reset launch) ----------
-// A tile's status word: epoch << 48 | flag << 46 | value (46 bits); flag 1 =
-// the tile's aggregate, 2 = its inclusive prefix. A word of another epoch is
-// unpublished, so the context's buffer is never cleared between launches
-// (lb_status hands out a new 16-bit epoch per launch). The word before the
-// status words counts tickets: tiles take them in the order they start (so a
-// tile only waits on tiles already running), and the tile that takes the
-// launch's last ticket sets the counter back to 0 for the next launch on the
-// stream (a compare-and-swap ticket on an epoch-tagged word instead cost
-// 40x: thousands of workgroups retrying on one address).
+// A tile's status is two words, each epoch << 48 | flag << 46 | 46 bits: the
+// value's low 46 bits in word 2t, its high 18 bits in word 2t + 1 (the full
+// 64-bit value: sums wrap mod 2^64 exactly like the reference's int64 sums,
+// ColumnReader.cc:960-993, and a corrupt length cannot silently lose its high
+// bits). Flag 1 = the tile's aggregate, 2 = its inclusive prefix; a tile
+// publishes each flag once per epoch, so two words carrying the same epoch
+// and flag belong to the same publication (no ordering between the two
+// stores or loads is needed; a reader that sees different flags retries). A
+// word of another epoch is unpublished, so the context's buffer is never
+// cleared between launches (lb_status hands out a new 16-bit epoch per
+// launch). The word before the status words counts tickets: tiles take them
+// in the order they start (so a tile only waits on tiles already running),
+// and the tile that takes the launch's last ticket sets the counter back to 0
+// for the next launch on the stream (a compare-and-swap ticket on an
+// epoch-tagged word instead cost 40x: thousands of workgroups retrying on one
+// address).
 constexpr uint64_t kLbMask = (1ull << 46) - 1;
+constexpr uint32_t kLbWords = 2;  // status words per tile
 
 __device__ __forceinline__ uint32_t lb_ticket(unsigned long long* status, uint32_t ntiles) {
   unsigned int* ctr = (unsigned int*)(status - 1);
@@ -61,9 +69,20 @@ __device__ __forceinline__ uint32_t lb_ticket(unsigned long long* status, uint32
 
 __device__ __forceinline__ void lb_publish(unsigned long long* status, uint32_t t, uint32_t flag, uint64_t v,
                                            uint32_t epoch) {
-  __hip_atomic_store(&status[t],
-                     ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46) | (v & kLbMask),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long tag = ((unsigned long long)epoch << 48) | ((unsigned long long)flag << 46);
+  __hip_atomic_store(&status[kLbWords * t], tag | (v & kLbMask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&status[kLbWords * t + 1], tag | (v >> 46), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Tile k's status: its flag (0 = not published in this epoch, or the two
+// words from different publications) and value.
+__device__ __forceinline__ uint32_t lb_read(unsigned long long* status, int64_t k, uint32_t epoch, uint64_t* v) {
+  const unsigned long long lo = __hip_atomic_load(&status[kLbWords * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long hi =
+      __hip_atomic_load(&status[kLbWords * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *v = (uint64_t)(lo & kLbMask) | ((uint64_t)(hi & kLbMask) << 46);
+  const bool same = (lo >> 46) == (hi >> 46) && (uint32_t)(lo >> 48) == epoch;
+  return same ? (uint32_t)((lo >> 46) & 3u) : 0u;
 }
 
 // One wave of tile t > 0 (after it published its aggregate): the sum over
@@ -72,22 +91,18 @@ __device__ uint64_t lb_lookback(unsigned long long* status, uint32_t t, uint32_t
   uint64_t excl = 0;
   for (int64_t j = (int64_t)t - 1;; j -= kWave) {
     const int64_t k = j - lane;
-    unsigned long long st = 0;
+    uint64_t v = 0;
     uint32_t fl = 2;  // before tile 0: an inclusive prefix of 0
-    if (k >= 0) {
-      st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      fl = (uint32_t)(st >> 48) == epoch ? (uint32_t)((st >> 46) & 3u) : 0u;
-    }
+    if (k >= 0) fl = lb_read(status, k, epoch, &v);
     while (__ballot(fl == 0) != 0) {
       if (fl == 0) {
         __builtin_amdgcn_s_sleep(1);
-        st = __hip_atomic_load(&status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fl = (uint32_t)(st >> 48) == epoch ? (uint32_t)((st >> 46) & 3u) : 0u;
+        fl = lb_read(status, k, epoch, &v);
       }
     }
     const uint64_t pm = __ballot(fl == 2);
     const int first = pm ? __builtin_ctzll(pm) : kWave;
-    uint64_t c = (k >= 0 && lane <= first) ? (uint64_t)(st & kLbMask) : 0ull;
+    uint64_t c = (k >= 0 && lane <= first) ? v : 0ull;
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
     excl += c;
@@ -515,6 +530,22 @@ __global__ void flag_negative_kernel(const int64_t* __restrict__ v, uint64_t n, 
   if (__any(neg) && (threadIdx.x % kWave) == 0) atomicOr(flag, 1ull);
 }
 
+// StringDirectColumnReader::computeSize's checks (ColumnReader.cc:694-710)
+// over a column's lengths and their exclusive scan: flags[0] |= 1 if a length
+// is negative, flags[1] |= 1 if the running total wraps (a start below its
+// predecessor: with non-negative lengths, the size_t total overflowed).
+__global__ void strlen_check_kernel(const int64_t* __restrict__ len, const int64_t* __restrict__ start, uint64_t n,
+                                    unsigned long long* flags) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  bool neg = false, wrap = false;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    neg |= len[i] < 0;
+    wrap |= (uint64_t)start[i + 1] < (uint64_t)start[i];
+  }
+  if (__any(neg) && (threadIdx.x % kWave) == 0) atomicOr(flags, 1ull);
+  if (__any(wrap) && (threadIdx.x % kWave) == 0) atomicOr(flags + 1, 1ull);
+}
+
 // ---- row-index segmentation (ColumnReader::seekToRowGroup positions) ----
 // A column's streams are cut at its row groups: the row index gives, per row
 // group g and stream, the run-aligned byte offset of the run holding the row
@@ -823,7 +854,7 @@ int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_
   if (!three) {
     unsigned long long* d_status;
     uint32_t epoch;
-    const int rc = lb_status(ctx, tiles + 1, &d_status, &epoch);
+    const int rc = lb_status(ctx, kLbWords * (tiles + 1), &d_status, &epoch);
     if (rc) return rc;
     hipLaunchKernelGGL(scan_lookback_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n, d_out,
                        d_status, (uint32_t)tiles, epoch);
@@ -865,6 +896,15 @@ int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_f
   hipLaunchKernelGGL(flag_negative_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_v, n,
                      (unsigned long long*)d_flag);
   return hip_check(ctx, hipGetLastError(), "flag launch");
+}
+
+int launch_strlen_check(Ctx* ctx, const int64_t* d_len, const int64_t* d_start, uint64_t n, uint64_t* d_flags) {
+  int rc = hip_check(ctx, hipMemsetAsync(d_flags, 0, 2 * sizeof(uint64_t), ctx->stream), "flag memset");
+  if (rc || n == 0) return rc;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(strlen_check_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_len, d_start, n,
+                     (unsigned long long*)d_flags);
+  return hip_check(ctx, hipGetLastError(), "string length check launch");
 }
 
 // A small host -> device copy by the shader: the workgroups read the pinned,
@@ -936,7 +976,7 @@ int launch_rg_prefix_segtab(Ctx* ctx, const uint8_t* d_mask, uint64_t n, const i
   if (G > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many row groups");
   unsigned long long* d_status;
   uint32_t epoch;
-  const int rc = lb_status(ctx, G + 1, &d_status, &epoch);
+  const int rc = lb_status(ctx, kLbWords * (G + 1), &d_status, &epoch);
   if (rc) return rc;
   hipLaunchKernelGGL(rg_prefix_segtab_kernel, dim3((unsigned)G), dim3(kThreads), 0, ctx->stream, d_mask, n, d_rows, G,
                      d_trip, boolean ? 1 : 0, d_prefix, d_seg, d_status, epoch);

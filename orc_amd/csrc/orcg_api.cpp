@@ -335,9 +335,9 @@ int orcg_ctx_create(int device, orcg_ctx** out) {
   if (warm) {
     std::lock_guard<std::mutex> lk(warm_mu);
     if (std::find(warmed.begin(), warmed.end(), device) == warmed.end()) {
-      warmed.push_back(device);
       orcg::warm_rlev2_walk(c->stream);
       orcg::warm_rlev2_tiled(c->stream);
+      orcg::warm_rlev2_expand(c->stream);
       orcg::warm_byterle(c->stream);
       orcg::warm_columns(c->stream);
       orcg::warm_rlev1(c->stream);
@@ -376,6 +376,9 @@ int orcg_ctx_create(int device, orcg_ctx** out) {
         orcg_ctx_destroy(c);
         return ORCG_DEVICE_ERROR;
       }
+      // only a warm-up that completed marks the device (a failed one is
+      // retried by the next context)
+      warmed.push_back(device);
     }
   }
   *out = c;
@@ -400,6 +403,8 @@ void orcg_ctx_destroy(orcg_ctx* c) {
   if (c->d_err) hipFree(c->d_err);
   if (c->d_defer) hipFree(c->d_defer);
   if (c->d_lb) hipFree(c->d_lb);
+  if (c->d_rtab) hipFree(c->d_rtab);
+  if (c->d_rhdr) hipFree(c->d_rhdr);
   if (c->d_jobs) hipFree(c->d_jobs);
   if (c->h_jobs) hipHostFree(c->h_jobs);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -758,4 +763,12 @@ extern "C" int orcg_debug_exclusive_scan(orcg_ctx* c, const int64_t* d_in, uint6
   if (!c || (n && !d_in) || !d_out) return ORCG_INVALID_ARGUMENT;
   hipSetDevice(c->device);
   return orcg::launch_exclusive_scan(c, d_in, n, d_out);
+}
+
+// Test hook: the next look-back launch on this context uses epoch `e` + 1
+// (tests/test_gpu_scan.py runs across the 16-bit epoch wrap in a few launches).
+extern "C" int orcg_debug_set_lb_epoch(orcg_ctx* c, uint32_t e) {
+  if (!c || e > 0xffffu) return ORCG_INVALID_ARGUMENT;
+  c->lb_epoch = e;
+  return ORCG_OK;
 }

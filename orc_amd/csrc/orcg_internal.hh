@@ -58,6 +58,11 @@ struct Ctx {
   void* d_lb = nullptr;
   uint64_t lb_cap = 0;
   uint32_t lb_epoch = 0;
+  // two-pass RLEv2 run table and segment headers (RunTab), grow-only
+  void* d_rtab = nullptr;
+  uint64_t rtab_cap = 0;
+  void* d_rhdr = nullptr;
+  uint64_t rhdr_cap = 0;
   // job tables of multi-stream launches: a pinned host ring and its device
   // mirror, in bytes (stage_table)
   void* h_jobs = nullptr;
@@ -112,7 +117,7 @@ struct RleJob {
   uint64_t nvalues;
   uint64_t seg_base;
   uint32_t is_signed;
-  uint32_t pad;
+  uint32_t tab_base;  // two-pass launches: the job's first run-table entry (set by the launcher)
   unsigned long long* err;  // the job's device error record (the reader's per-column word), or null = the launch's
   const uint64_t* dcount;   // non-null: the value count on the device (nvalues is then the output's capacity)
 };
@@ -168,6 +173,32 @@ struct RowScatter {
   void* out;              // nrows elements of the decode's output type
 };
 
+// Two-pass short-run RLEv2 decode (DESIGN.md §3.1 "Two passes"): the union
+// instance's dense (short-run) passes write their run starts to `tab` instead
+// of expanding them, and rlev2_expand_kernel then expands every segment's
+// tabled runs in value slices of `slice` values (spg slices per segment), a
+// workgroup per slice. Per launch-wide segment g, hdr[g * (kRtHdr + spg) + i]:
+// [0] table entries, [1] values the passes reached (segment-relative), [2..3]
+// the segment's first value index, [4] its first table entry, [kRtHdr + k]
+// the entry to start slice k from (k >= 1), [5] the segment's job (multi-
+// stream launches). An entry is the run's stream byte
+// offset | its first value (segment-relative) << 32. Runs of passes the first
+// kernel expands itself (long runs, values past spg * slice) are not tabled.
+constexpr uint32_t kRtHdr = 6;
+constexpr uint32_t kSliceMax = 2048;
+struct RunTab {
+  uint64_t* tab;
+  uint32_t* hdr;
+  uint32_t spg;
+  uint32_t slice;
+};
+// The second pass over `nsegs` launch-wide segments (single stream: d_src ..
+// d_count as launch_rlev2_tiled; multi-stream: jobs_d, int64 output).
+int launch_rlev2_expand(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed, uint64_t value_begin,
+                        uint64_t nvalues, void* d_dst, int dst_bytes, const uint64_t* d_count, const RleJob* jobs_d,
+                        uint32_t njobs, uint64_t nsegs, const RunTab& rt);
+void warm_rlev2_expand(hipStream_t s);
+
 // RLEv2 kernel variants a context accepts (orcg_rlev2_variants): 0 default,
 // 1 wave-walk, and pins of single tiled instances (launch_rlev2_tiled).
 constexpr int kMaxRlev2Variant = 39;
@@ -205,6 +236,10 @@ struct MultiLaunch {
   uint32_t njobs;
   uint64_t grid;      // segments / tiles
   uint64_t values;
+  // two-pass RLEv2 launch (kind 0, spg > 0): run-table entries, slices per
+  // segment and values per slice (RunTab)
+  uint64_t tab_entries = 0;
+  uint32_t spg = 0, slice = 0;
 };
 int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<MultiLaunch>& out);
 int plan_rlev1_multi(Ctx* ctx, const V1SegDesc* segs, uint64_t nsegs, std::vector<MultiLaunch>& out);
@@ -290,6 +325,9 @@ int launch_union_offsets(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t k
 int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out);
 // Number of non-zero bytes of d_nn[0..n) into *d_total (device). Scratch 5, 6.
 int launch_count_nonzero(Ctx* ctx, const uint8_t* d_nn, uint64_t n, uint64_t* d_total);
+// StringDirect lengths and their exclusive scan (n + 1 starts): d_flags[0] =
+// 1 if a length is negative, d_flags[1] = 1 if the total wrapped, else 0.
+int launch_strlen_check(Ctx* ctx, const int64_t* d_len, const int64_t* d_start, uint64_t n, uint64_t* d_flags);
 // *d_flag = 1 if any d_v[i] < 0, else 0.
 int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_flag);
 enum WidenKind { kWidenI8 = 0, kWidenU8 = 1, kWidenF32 = 2 };

@@ -1331,10 +1331,24 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       StreamBuf& db = c.s[kSlotData];
       c.blob = D->d_stage + db.host_off;
       c.blob_len = db.len;
+      // computeSize's checks (ColumnReader.cc:694-710) in the reference's
+      // order: a negative length, the total's overflow, then the blob's size
+      const uint64_t* h_fl = nullptr;
+      uint64_t* flags = rb_alloc(2, &h_fl);
+      if (!flags) ORCG_ALLOC_TO(uint64_t, flags, 2);
+      if ((rc = launch_strlen_check(ctx, rows_placed ? placed : dlen, dstart, ns, flags))) return fail_ctx(rc);
+      if (!h_fl && !(h_fl = defer(flags, 2))) return fail(ORCG_DEVICE_ERROR, "D2H of the string length checks failed");
       const uint64_t* need = defer(dstart + ns, 1);
       if (!need) return fail(ORCG_DEVICE_ERROR, "D2H of the string bytes failed");
       const uint64_t blob_len = c.blob_len;
-      F->checks.emplace_back(cur_col, [this, need, blob_len]() -> int {
+      const uint32_t col_id = cur_col;
+      F->checks.emplace_back(cur_col, [this, need, blob_len, h_fl, col_id]() -> int {
+        if (h_fl[0])
+          return fail(ORCG_PARSE_ERROR,
+                      "Negative string length in StringDirectColumnReader for column " + std::to_string(col_id));
+        if (h_fl[1])
+          return fail(ORCG_PARSE_ERROR,
+                      "String length overflow in StringDirectColumnReader for column " + std::to_string(col_id));
         return *need > blob_len ? fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next") : ORCG_OK;
       });
       if (rows_placed) {

@@ -38,6 +38,9 @@ using namespace dev;
 // thread 0 adds the cycles between consecutive phase marks to g_phase[k].
 #ifdef ORCG_PHASE_PROF
 __device__ unsigned long long g_phase[16];
+// union instances: per workgroup {wall-clock ticks, dense passes | serial passes << 32}
+constexpr uint32_t kWgDurMax = 16384;
+__device__ unsigned long long g_wgdur[2 * kWgDurMax];
 #define PROF_MARK(k)                                                        \
   do {                                                                      \
     if (threadIdx.x == 0) {                                                 \
@@ -89,6 +92,17 @@ constexpr uint16_t kSink = 0xffffu;          // chain successor: none
 constexpr uint32_t kWalkDone = 0x80000000u;  // published-runs flag: the walk has finished
 // density hysteresis (stream bytes per run of the last pass)
 constexpr uint32_t kToDense = 24, kToSerial = 64;
+// two-pass (kOptTable) instances: dense discovery no longer pays for the
+// expansion, and a serial walk over medium runs (DELTA / DIRECT runs of tens
+// of bytes) was the launch's tail (one wave walking a whole row group while
+// co-resident workgroups share the CU): dense up to far longer runs
+#ifndef ORCG_TAB_TO_DENSE
+#define ORCG_TAB_TO_DENSE 128
+#endif
+#ifndef ORCG_TAB_TO_SERIAL
+#define ORCG_TAB_TO_SERIAL 512
+#endif
+constexpr uint32_t kTabToDense = ORCG_TAB_TO_DENSE, kTabToSerial = ORCG_TAB_TO_SERIAL;
 
 // kOpt bits
 constexpr int kOptNTStore = 1;  // non-temporal output stores (streamed, never re-read)
@@ -108,6 +122,8 @@ constexpr int kOptPrefetch = 2048;  // register-filled serial windows: every wav
                                     // into registers as soon as the walk is done, while it expands this one
 constexpr int kOptGrpT = 8192;      // serial groups of short runs (one lane per run, scattered 8-byte stores):
                                     // temporal stores, so L2 merges the partial lines before they reach HBM
+constexpr int kOptTable = 16384;    // two-pass (RunTab): dense passes write their runs to the run table for
+                                    // rlev2_expand_kernel instead of expanding them
 
 // Debug build only (ORCG_AB_FLAGS=-DORCG_DEBUG_COVER): every expansion path
 // counts the values of the runs it expands; each pass checks the count
@@ -1650,7 +1666,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint64_t* __restrict__ p_segtab, uint64_t p_nsegs, uint64_t rows_per_group,
     uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* p_err,
     unsigned long long* __restrict__ defer_q, uint32_t defer_par, const RleJob* __restrict__ jobs,
-    uint32_t njobs, const uint64_t* __restrict__ p_dcount, const RowScatter rsc) {
+    uint32_t njobs, const uint64_t* __restrict__ p_dcount, const RowScatter rsc, const RunTab rtab) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
@@ -1658,6 +1674,9 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   // union instances: serial windows of kWinS bytes = the dense window, its
   // 32-byte slack, the value stages and the marks
   constexpr bool kUnion = kDense == 2 && (kOpt & kOptUnion) != 0;
+  // density hysteresis (stream bytes per run)
+  constexpr uint32_t kDenseB = (kOpt & kOptTable) ? kTabToDense : kToDense;
+  constexpr uint32_t kSerialB = (kOpt & kOptTable) ? kTabToSerial : kToSerial;
   constexpr uint32_t kWinS = kUnion ? kWin + (uint32_t)(kWaves * kStage * 8 + kSlab / 8) : kWin;
   constexpr uint32_t kChunkS = kWinS - kMaxRun;
   static_assert(!kUnion || (kWin + 32) % 8 == 0, "stage alignment");
@@ -1712,6 +1731,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
 
   const int tid = (int)threadIdx.x;
   const int wave = tid / kWave, lane = tid % kWave;
+#ifdef ORCG_PHASE_PROF
+  const uint64_t wg_t0 = wall_clock64();
+  uint32_t wg_dense = 0, wg_serial = 0;
+#endif
   // the stream of the segment being decoded: the launch's, or (multi-stream
   // instances, kMulti) the job of `jobs` that owns the launch-wide segment
   // index (single-stream instances never rebind: the arguments stay as they
@@ -1730,6 +1753,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   uint64_t value_end = p_value_begin + (p_dcount ? uni64(*p_dcount) : p_nvalues);
   T* dst = p_dst;
   unsigned long long* err = p_err;
+  uint32_t tab_base = 0;  // kOptTable: the stream's first run-table entry
+  uint32_t job_idx = 0;   // kMulti: the segment's job
   auto bind = [&](const uint64_t gg) -> uint64_t {
     if constexpr (!kMulti) return gg;
     uint32_t lo = 0, hi = njobs - 1;
@@ -1752,6 +1777,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     dst = (T*)uni64((uint64_t)(uintptr_t)J->dst);
     const uint64_t je = uni64((uint64_t)(uintptr_t)J->err);
     err = je ? (unsigned long long*)(uintptr_t)je : p_err;
+    tab_base = uni(J->tab_base);
+    job_idx = lo;
     return gg - uni64(J->seg_base);
   };
 
@@ -1778,6 +1805,27 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   uint64_t v_next = ~0ull;
   if (g + 1 < nsegs) v_next = seg_at(g + 1, &seg_end);
   if (seg_end > src_len) seg_end = src_len;
+  // kOptTable: the segment's header and run table (RunTab). Its runs lie in
+  // [seg_first, next segment's first byte) and are >= 2 bytes each, so
+  // seg_first / 2 + g leaves every earlier segment room for its runs.
+  constexpr bool kTable = (kOpt & kOptTable) != 0;
+  uint32_t* thdr = nullptr;
+  uint64_t* ttab = nullptr;
+  uint32_t tcnt = 0;                                     // entries written
+  const uint64_t tlim = (uint64_t)rtab.spg * rtab.slice;  // values the slices cover
+  if constexpr (kTable) {
+    thdr = rtab.hdr + gg * (kRtHdr + rtab.spg);
+    const uint32_t tb = tab_base + (uint32_t)(seg_first >> 1) + (uint32_t)g;
+    ttab = rtab.tab + tb;
+    if (tid == 0) {
+      thdr[0] = 0;
+      thdr[1] = 0;
+      thdr[2] = (uint32_t)vi0;
+      thdr[3] = (uint32_t)(vi0 >> 32);
+      thdr[4] = tb;
+      thdr[5] = job_idx;
+    }
+  }
   if (vi >= value_end || v_next <= value_begin) return;
   if (seg_start >= seg_end) {
     if (tid == 0 && v_next != ~0ull && v_next != vi && seg_start < src_len) report(err, vi, kErrBadSegment);
@@ -1893,14 +1941,14 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         if (probe) {
           if (tid == 0) {
             uint32_t p = (uint32_t)(pos - wpos), nb = 0, nr = 0;
-            while (nr < 4 && nb < 4 * kToDense && p + kHdrLim < need) {
+            while (nr < 4 && nb < 4 * kDenseB && p + kHdrLim < need) {
               const Run r = parse_run([&](uint32_t i) { return lds_byte(s_win[0], p + i); }, ~0ull, kHdrLim, is_signed);
               if (r.err != kErrNone || r.kind == 2) break;
               nb += r.bytes;
               p += r.bytes;
               ++nr;
             }
-            s_ctl[0][15] = (nr == 4 && nb < 4 * kToDense) ? 1u : 0u;
+            s_ctl[0][15] = (nr == 4 && nb < 4 * kDenseB) ? 1u : 0u;
           }
           __syncthreads();
           dense = uni(s_ctl[0][15]) != 0;
@@ -1916,6 +1964,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         __syncthreads();
 #endif
         bool was_dense = false;
+        bool tabled = false;  // kOptTable: this pass's runs went to the run table
         if constexpr (kDense) was_dense = dense;
         if (was_dense) {
           const uint32_t sb = (uint32_t)(pos - wpos);
@@ -1941,13 +1990,34 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           stop = d.stop;
           dpos = d.dpos;
           dval = d.dval;
+          if constexpr (kTable) {
+            // the runs go to the run table (entry: stream byte offset | first
+            // value in the segment << 32); a run holding slice boundary k * S
+            // is where slice k starts (runs are <= 512 < S values: one each)
+            const uint64_t vrel = vi - vi0;
+            if (vrel + dval <= tlim) {
+              tabled = true;
+              const uint32_t vr = (uint32_t)vrel, S = rtab.slice;
+              for (uint32_t r = (uint32_t)tid; r < n; r += kThreads) {
+                const uint32_t v = vr + s_val[0][r];
+                const uint32_t ve = vr + (r + 1 < n ? s_val[0][r + 1] : dval);
+                ttab[tcnt + r] = (wpos + s_off[0][r]) | ((uint64_t)v << 32);
+                const uint32_t kb = (v + S - 1) / S;
+                if (kb >= 1 && kb * S < ve) thdr[kRtHdr + kb] = tcnt + r;
+              }
+              tcnt += n;
+            }
+          }
           if constexpr (kDense != 0) {
-            uint64_t* stage;
-            if constexpr (kDense == 2) stage = s_stage2 + wave * kStage;
-            else stage = s_dense.stage[wave];
-            const uint32_t r0 = (uint32_t)(((uint64_t)n * wave) / kWaves), r1 = (uint32_t)(((uint64_t)n * (wave + 1)) / kWaves);
-            dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], stage, r0, r1, vi, is_signed,
-                               value_begin, value_end, dst, lane);
+            if (!tabled) {
+              uint64_t* stage;
+              if constexpr (kDense == 2) stage = s_stage2 + wave * kStage;
+              else stage = s_dense.stage[wave];
+              const uint32_t r0 = (uint32_t)(((uint64_t)n * wave) / kWaves),
+                             r1 = (uint32_t)(((uint64_t)n * (wave + 1)) / kWaves);
+              dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], stage, r0, r1, vi, is_signed,
+                                 value_begin, value_end, dst, lane);
+            }
           }
         } else {
           // Wave 0 walks and publishes work items (a group of short runs or
@@ -2069,6 +2139,24 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
         __syncthreads();
 #endif
         PROF_MARK(was_dense ? 6 : 2);
+#ifdef ORCG_PHASE_PROF
+        if (was_dense) ++wg_dense;
+        else ++wg_serial;
+#endif
+        if constexpr (kTable) {
+          // a pass expanded here: slices starting inside it start at the next
+          // table entry; then the segment header (read by the second pass)
+          const uint64_t vrel = vi - vi0, vend = vrel + dval;
+          if (!tabled) {
+            const uint64_t S = rtab.slice, ve = vend < tlim ? vend : tlim;
+            const uint64_t kb0 = vrel == 0 ? 1u : (vrel + S - 1) / S;
+            for (uint64_t kb = kb0 + (uint64_t)tid; kb * S < ve; kb += kThreads) thdr[kRtHdr + kb] = tcnt;
+          }
+          if (tid == 0) {
+            thdr[0] = tcnt;
+            thdr[1] = vend < 0xffffffffull ? (uint32_t)vend : 0xffffffffu;
+          }
+        }
         if (stop) return;
         pos += dpos;
         vi += dval;
@@ -2101,8 +2189,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           // hysteresis on the stream bytes per run of this pass
           if (n > 0) {
             const uint32_t bpr = dpos / n;
-            if (shrt || (!dense && (n >= 8 || (was_probe && n >= 4)) && bpr < kToDense)) dense = true;
-            else if (dense && bpr >= kToSerial) dense = false;
+            if (shrt || (!dense && (n >= 8 || (was_probe && n >= 4)) && bpr < kDenseB)) dense = true;
+            else if (dense && bpr >= kSerialB) dense = false;
           }
         }
         if (n == 0 && dpos == 0) break;  // nothing consumed (cannot happen for a good window)
@@ -2198,6 +2286,12 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     run_segment(blockIdx.x, false, 0, 0);
     if (!seg_queued) place(blockIdx.x);
   }
+#ifdef ORCG_PHASE_PROF
+  if (kUnion && tid == 0 && blockIdx.x < kWgDurMax) {
+    g_wgdur[2 * blockIdx.x] = wall_clock64() - wg_t0;
+    g_wgdur[2 * blockIdx.x + 1] = wg_dense | ((uint64_t)wg_serial << 32);
+  }
+#endif
 }
 
 }  // namespace
@@ -2208,11 +2302,11 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
 // tuning experiments of the A/B sweeps (8-24) are compiled only into the A/B
 // build (ORCG_AB=1 python -m orc_amd.build -> liborcgpu_ab.so).
 bool rlev2_variant_valid(int v) {
-  if (v >= 0 && v <= 7) return true;
+  if (v >= 0 && v <= 8) return true;
 #ifdef ORCG_AB_VARIANTS
   // 28-30 (value-parallel short-run groups) were dropped: wrong on short
   // runs of wide values (tests/test_gpu_dense.py test_wide_short_runs_vs_oracle)
-  if (v >= 8 && v <= kMaxRlev2Variant && (v < 28 || v > 30)) return true;
+  if (v >= 9 && v <= kMaxRlev2Variant && (v < 28 || v > 30)) return true;
 #endif
   return false;
 }
@@ -2255,7 +2349,8 @@ static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
 // ones (at 6 WG/CU they carry 56 B/lane of scratch, the serial ones none), so long-run
 // streams above 1.25 B/value stay on the serial instance.
 static int default_variant(uint64_t src_len, uint64_t est_values) {
-  return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 6);
+  static const int uv = getenv("ORCG_ONE_PASS") ? 8 : 6;  // TEMP A/B
+  return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : uv);
 }
 
 // One launch (or serial + drain pair) of instance `variant` over nsegs
@@ -2276,12 +2371,87 @@ static void debug_defer(Ctx* ctx, const unsigned long long* dq, uint64_t nsegs, 
           (unsigned long long)nsegs, h[3 * nsegs] == dpar ? 1 : 0);
 }
 
+// Two-pass shape for segments of at most `seg_values` values (a bound: a
+// segment that turns out longer has its later passes expanded by the first
+// kernel): slices of <= kSliceMax values, a multiple of 256, spg per segment.
+static void two_pass_shape(uint64_t seg_values, uint32_t* spg, uint32_t* slice) {
+  const uint64_t n = std::max<uint64_t>(seg_values, 1);
+  const uint64_t k = std::min<uint64_t>((n + kSliceMax - 1) / kSliceMax, 256);
+  uint64_t s = (n + k - 1) / k;
+  s = std::min<uint64_t>((s + 255) & ~255ull, kSliceMax);
+  *spg = (uint32_t)k;
+  *slice = (uint32_t)s;
+}
+
+// A segment's value bound for the two-pass shape: its share of the values,
+// + 1/8 and one run (row-index segments start up to 511 values early).
+static uint64_t seg_value_bound(uint64_t values, uint64_t nsegs) {
+  const uint64_t avg = (values + nsegs - 1) / std::max<uint64_t>(nsegs, 1);
+  return avg + avg / 8 + 512;
+}
+
+// The context's run table (entries) and segment headers (nsegs x (kRtHdr +
+// spg) words), grow-only; nothing needs clearing (the first kernel writes
+// every segment's header before the second reads it).
+static int runtab_buffers(Ctx* ctx, uint64_t entries, uint64_t nsegs, uint32_t spg, uint32_t slice, RunTab* rt) {
+  const uint64_t tb = std::max<uint64_t>(entries, 1) * 8, hb = nsegs * (kRtHdr + spg) * 4;
+  if (ctx->rtab_cap < tb || ctx->rhdr_cap < hb) {
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->rtab_cap < tb) {
+      if (ctx->d_rtab) (void)hipFree(ctx->d_rtab);
+      ctx->d_rtab = nullptr;
+      ctx->rtab_cap = 0;
+      const uint64_t cap = std::max<uint64_t>(tb + tb / 4, 1u << 20);
+      int rc = hip_check(ctx, hipMalloc(&ctx->d_rtab, cap), "hipMalloc run table");
+      if (rc) return rc;
+      ctx->rtab_cap = cap;
+    }
+    if (ctx->rhdr_cap < hb) {
+      if (ctx->d_rhdr) (void)hipFree(ctx->d_rhdr);
+      ctx->d_rhdr = nullptr;
+      ctx->rhdr_cap = 0;
+      const uint64_t cap = std::max<uint64_t>(hb + hb / 4, 256u << 10);
+      int rc = hip_check(ctx, hipMalloc(&ctx->d_rhdr, cap), "hipMalloc run-table headers");
+      if (rc) return rc;
+      ctx->rhdr_cap = cap;
+    }
+  }
+  *rt = RunTab{(uint64_t*)ctx->d_rtab, (uint32_t*)ctx->d_rhdr, spg, slice};
+  return ORCG_OK;
+}
+
 static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode, uint64_t rows_per_group,
                         uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes, const RleJob* jobs_d,
-                        uint32_t njobs_d, const uint64_t* dcount = nullptr, const RowScatter* rsc_p = nullptr) {
+                        uint32_t njobs_d, const uint64_t* dcount = nullptr, const RowScatter* rsc_p = nullptr,
+                        const MultiLaunch* ml = nullptr) {
   if (nsegs == 0 || nvalues == 0) return ORCG_OK;
   const RowScatter rsc = rsc_p ? *rsc_p : RowScatter{};
+  RunTab rtab{nullptr, nullptr, 0, 0};
+  if (variant == 6) {
+    // the union instance in two passes, when the run table can address the
+    // stream (u32 entries and offsets) and no in-decode placement is asked
+    // for (RowScatter reads the values the first kernel no longer writes)
+    uint64_t entries = 0, bound = 0;
+    uint32_t spg = 0, slice = 0;
+    if (jobs_d) {
+      if (ml && ml->spg) {
+        entries = ml->tab_entries;
+        spg = ml->spg;
+        slice = ml->slice;
+      }
+    } else if (!rsc.out && src_len < 0xffff0000ull && nsegs < 0x7fff0000ull) {
+      entries = src_len / 2 + nsegs + 1;
+      bound = positions_mode ? rows_per_group + 512 : seg_value_bound(nvalues, nsegs);
+      two_pass_shape(bound, &spg, &slice);
+    }
+    if (spg && entries < 0xffff0000ull && nsegs * spg < 0x7fffffffull) {
+      const int rc = runtab_buffers(ctx, entries, nsegs, spg, slice, &rtab);
+      if (rc) return rc;
+    } else {
+      variant = 8;  // one pass
+    }
+  }
   if (rsc.out && (jobs_d || positions_mode || value_begin))
     return set_error(ctx, ORCG_INVALID_ARGUMENT, "row placement needs a single-stream segment-table launch");
   if (rsc.out && ((uintptr_t)rsc.mask & 15u))
@@ -2303,7 +2473,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
   hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
                      d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
-                     ctx->d_err, dq, dpar, jobs_d, njobs_d, dcount, rsc)
+                     ctx->d_err, dq, dpar, jobs_d, njobs_d, dcount, rsc, rtab)
 // single-stream instances (+ the multi-stream one for the default's
 // instances, ORCG_KX; the tuning variants have none, ORCG_KX1)
 #define ORCG_KX1(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                 \
@@ -2365,10 +2535,18 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     case 3: ORCG_DEFERRING(kSer | kOptD3, 21, 6, kSer | kOptD3); break;   // 21 KB serial + dense drain
     case 4: ORCG_KX(kSer | kOptD3, 8, false, 6, 2, 0, grid_s); break;   // dense v3, 8.5 KB
     case 5: ORCG_KX(kSer | kOptD3, 12, false, 5, 2, 0, grid_s); break;  // dense v3, 12.5 KB
-    case 6: ORCG_KX(kSer | kOptD3 | kOptUnion, 8, false, 6, 2, 0, grid_s); break;  // union: dense 8.5 KB / serial 16.75 KB windows
+    case 6: {
+      // union, two passes: dense passes table their runs, rlev2_expand_kernel
+      // expands them in value slices
+      ORCG_KX(kSer | kOptD3 | kOptUnion | kOptTable, 8, false, 6, 2, 0, grid_s);
+      const int rc = hip_check(ctx, hipGetLastError(), "rlev2_tiled_kernel launch");
+      if (rc) return rc;
+      return launch_rlev2_expand(ctx, d_src, src_len, sg, value_begin, nvalues, d_dst, dst_bytes, dcount, jobs_d,
+                                 njobs_d, nsegs, rtab);
+    }
     case 7: ORCG_DEFERRING(kWide | kOptD3, 33, 1, kSer | kOptD3); break;  // 33 KB serial + dense drain (round-3 default, A/B)
+    case 8: ORCG_KX(kSer | kOptD3 | kOptUnion, 8, false, 6, 2, 0, grid_s); break;  // union in one pass (round-5 default)
 #ifdef ORCG_AB_VARIANTS
-    case 8: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 21, false, 6, false); break;  // 21 KB + fast
     case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
     case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 20, false, 4, true); break;  // dense v1, 20.5 KB
     case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 12, false, 5, true); break;  // dense v1, 12.5 KB
@@ -2455,7 +2633,7 @@ int stage_table(Ctx* ctx, const void* src, size_t bytes, const void** out) {
   return hip_check(ctx, hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, ctx->stream), "H2D jobs");
 }
 
-bool rlev2_multi_capable(int variant) { return variant == 0 || (variant >= 2 && variant <= 7); }
+bool rlev2_multi_capable(int variant) { return variant == 0 || (variant >= 2 && variant <= 8); }
 
 int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<MultiLaunch>& out) {
   const int pinned = ctx->rlev2_variant;
@@ -2469,7 +2647,7 @@ int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<M
     return ORCG_OK;
   }
   // one launch per instance: group the streams by the instance they get
-  std::vector<RleJob> group[8];
+  std::vector<RleJob> group[9];
   for (uint32_t j = 0; j < njobs; ++j) {
     const RleJob& J = jobs[j];
     if (J.nsegs == 0 || J.nvalues == 0) continue;
@@ -2477,12 +2655,12 @@ int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<M
   }
   static const bool dbg = getenv("ORCG_DEBUG_JOBS") != nullptr;
   if (dbg)
-    for (int v = 2; v <= 7; ++v)
+    for (int v = 2; v <= 8; ++v)
       for (const RleJob& J : group[v])
         fprintf(stderr, "rle job: instance %d bytes %llu values %llu segments %llu (%.3f B/value)\n", v,
                 (unsigned long long)J.src_len, (unsigned long long)J.nvalues, (unsigned long long)J.nsegs,
                 (double)J.src_len / (double)J.nvalues);
-  for (int v = 2; v <= 7; ++v) {
+  for (int v = 2; v <= 8; ++v) {
     std::vector<RleJob>& g = group[v];
     if (g.empty()) continue;
     // workgroups start in index order: the streams with the most stream
@@ -2491,17 +2669,26 @@ int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<M
     std::stable_sort(g.begin(), g.end(), [](const RleJob& a, const RleJob& b) {
       return (double)a.src_len * (double)b.nvalues > (double)b.src_len * (double)a.nvalues;
     });
-    uint64_t segs = 0, values = 0;
+    uint64_t segs = 0, values = 0, entries = 0, bound = 0;
     for (RleJob& J : g) {
       J.seg_base = segs;
       segs += J.nsegs;
       values += J.nvalues;
+      // two-pass (the union instance): the job's run-table range
+      J.tab_base = (uint32_t)std::min<uint64_t>(entries, 0xffffffffull);
+      entries += J.src_len / 2 + J.nsegs + 1;
+      bound = std::max(bound, seg_value_bound(J.nvalues, J.nsegs));
     }
     if (segs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
     const RleJob* d = nullptr;
     const int rc = stage_rle_jobs(ctx, g.data(), (uint32_t)g.size(), &d);
     if (rc) return rc;
-    out.push_back(MultiLaunch{0, v, d, (uint32_t)g.size(), segs, values});
+    MultiLaunch m{0, v, d, (uint32_t)g.size(), segs, values};
+    if (v == 6 && entries < 0xffff0000ull) {
+      m.tab_entries = entries;
+      two_pass_shape(bound, &m.spg, &m.slice);
+    }
+    out.push_back(m);
   }
   return ORCG_OK;
 }
@@ -2546,7 +2733,7 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
       unsigned long long* const own = c->d_err;
       c->d_err = base->d_err;
       rc = launch_tiled(c, m.variant, nullptr, 0, 0, nullptr, m.grid, false, 0, 0, m.values, nullptr, 8,
-                        (const RleJob*)m.d_jobs, m.njobs);
+                        (const RleJob*)m.d_jobs, m.njobs, nullptr, nullptr, &m);
       c->d_err = own;
       if (rc) {
         char b[160];
@@ -2583,6 +2770,11 @@ int launch_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs) {
 }  // namespace orcg
 
 #ifdef ORCG_PHASE_PROF
+extern "C" int orcg_debug_wg_durations(unsigned long long* out, int n) {
+  if (n > (int)(2 * orcg::kWgDurMax)) n = 2 * orcg::kWgDurMax;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(orcg::g_wgdur), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+
 extern "C" int orcg_debug_phase_counters(unsigned long long* out, int n, int reset) {
   unsigned long long h[16];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(orcg::g_phase), sizeof(h)) != hipSuccess) return -1;

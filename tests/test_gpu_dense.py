@@ -17,8 +17,10 @@ pytestmark = pytest.mark.gpu
 # default (three density tiers: 33 KB serial, 21 KB serial + queue, union), the 33 KB serial instance,
 # the 21 KB serial instance that queues short-run segments, the dense
 # instances (8.5 KB, 12.5 KB), the union instance (8.5 KB dense / 16.75 KB
-# serial windows), the 33 KB serial instance that queues
-DENSE_VARIANTS = [0, 2, 3, 4, 5, 6, 7]
+# serial windows) in two passes (its dense passes table their runs, the
+# expansion kernel expands them by value slices), the 33 KB serial instance
+# that queues, the union instance in one pass
+DENSE_VARIANTS = [0, 2, 3, 4, 5, 6, 7, 8]
 # A/B instances of the tuning build (ORCG_LIB=liborcgpu_ab.so), e.g.
 # ORCG_TEST_EXTRA_VARIANTS=34,35
 DENSE_VARIANTS += [int(v) for v in os.environ.get("ORCG_TEST_EXTRA_VARIANTS", "").split(",") if v]
@@ -339,5 +341,106 @@ def test_value_parallel_expansion_vs_oracle(bits, signed):
                 i = int(np.flatnonzero(got != want)[0])
                 raise AssertionError("variant %d: first mismatch at %d: got %s want %s" % (
                     variant, i, got[max(0, i - 4):i + 8].tolist(), want[max(0, i - 4):i + 8].tolist()))
+    finally:
+        ctx.set_rlev2_variant(0)
+
+
+def _skew_stream(rng, signed, n_target, long_kind, every):
+    """Short-run row groups (SHORT_REPEAT runs of 3 values) with one long run
+    of `long_kind` every `every` short runs: DIRECT runs of 512 values, DELTA
+    runs of 200-512 values with variable deltas, or PATCHED_BASE runs of
+    100-512 values. The stream stays dense (few bytes per run on average), so
+    the long runs land in tabled dense passes and cross value slices."""
+    vals, kinds, lens = [], [], []
+    total, i = 0, 0
+    while total < n_target:
+        i += 1
+        if i % every == 0:
+            if long_kind == "direct":
+                k, L = 1, 512
+                hi = 1 << 6
+                v = [int(x) for x in rng.integers(-hi if signed else 0, hi, size=L)]
+            elif long_kind == "delta":
+                k, L = 3, int(rng.integers(200, 513))
+                start = int(rng.integers(-10 ** 6, 10 ** 6)) if signed else int(rng.integers(10 ** 7, 2 * 10 ** 7))
+                d = rng.integers(0, 100, size=L)
+                d[0] = 0
+                sgn = -1 if (signed and rng.integers(0, 2)) else 1
+                if not signed:
+                    sgn = 1 if rng.integers(0, 2) else -1
+                d[1] = max(int(d[1]), 1)
+                v = [int(x) for x in start + sgn * np.cumsum(d)]
+            else:
+                k, L = 2, int(rng.integers(100, 513))
+                base = int(rng.integers(0, 5000))
+                x = base + rng.integers(0, 200, size=L)
+                npatch = int(rng.integers(1, 6))
+                idx = rng.choice(L, size=npatch, replace=False)
+                x[idx] += rng.integers(1 << 20, 1 << 30, size=npatch)
+                v = [int(y) for y in x]
+        else:
+            k, L = 0, 3
+            x = int(rng.integers(-300, 300)) if signed else int(rng.integers(0, 1 << 12))
+            v = [x] * L
+        vals += v
+        kinds.append(k)
+        lens.append(L)
+        total += L
+    return np.array(vals, dtype=np.int64), np.array(kinds, dtype=np.uint8), np.array(lens, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("long_kind", ["direct", "delta", "patched"])
+@pytest.mark.parametrize("signed", [True, False])
+def test_two_pass_skew_vs_oracle(long_kind, signed):
+    """The two-pass union decode (variant 6; rlev2_tiled.hip kOptTable +
+    rlev2_expand.hip) on row groups that mix 3-value SHORT_REPEAT runs with
+    long DIRECT / variable-width DELTA / PATCHED_BASE runs: the long runs sit
+    in tabled dense passes and straddle value slices (a DELTA run begun before
+    its slice is resumed from its running sum), at row-group strides that cut
+    segments mid-run and with row ranges; bit-exact against the oracle
+    (RleDecoderV2.cc:184-248, 250-370, 372-435) and against the one-pass
+    union instance (variant 8)."""
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(101 + 7 * len(long_kind) + int(signed))
+    every = 60 if long_kind == "direct" else 25
+    v, kinds, lens = _skew_stream(rng, signed, 500_000, long_kind, every)
+    ctx = orc_amd.default_context(0)
+    try:
+        for stride in (10_000, 3_333, 50_000):
+            data, pos = _encode_with_positions(orc_amd, v, signed, kinds, lens, stride)
+            assert data.size < 1.25 * v.size  # the default's union tier
+            if stride == 10_000:
+                want = oracle.rlev2_decode(data.tobytes(), v.size, signed)
+                np.testing.assert_array_equal(want, v)
+            d_src = torch.from_numpy(data).cuda()
+            d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+            for variant in (0, 6, 8):
+                ctx.set_rlev2_variant(variant)
+                out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
+                orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, signed, out)
+                ctx.synchronize()
+                got = out.cpu().numpy()
+                if not np.array_equal(got, v):
+                    i = int(np.flatnonzero(got != v)[0])
+                    raise AssertionError("variant %d stride %d: first mismatch at %d: got %s want %s" % (
+                        variant, stride, i, got[max(0, i - 4):i + 8].tolist(), v[max(0, i - 4):i + 8].tolist()))
+        # segment tables (host plans) and a row range inside the stream
+        data, _ = orc_amd.encode_runs(v, signed, kinds, lens)
+        d_src = torch.from_numpy(data).cuda()
+        plan = orc_amd.Plan(data, 8 << 10, 8192)
+        d_seg = torch.from_numpy(plan.segments().view(np.int64)).cuda()
+        for variant in (6, 8):
+            ctx.set_rlev2_variant(variant)
+            for a, b in ((0, v.size), (12_345, 400_001)):
+                out = torch.zeros(b - a, dtype=torch.int64, device="cuda")
+                orc_amd.decode_device(ctx, d_src, d_seg, b - a, signed, out, value_begin=a)
+                ctx.synchronize()
+                got = out.cpu().numpy()
+                if not np.array_equal(got, v[a:b]):
+                    i = int(np.flatnonzero(got != v[a:b])[0])
+                    raise AssertionError("variant %d plan range %d-%d: first mismatch at %d" % (variant, a, b, a + i))
     finally:
         ctx.set_rlev2_variant(0)
