@@ -190,6 +190,27 @@ int orcg_rle_decoder_next_vector_java(orcg_rle_decoder* dec, int64_t* vector, co
 int orcg_rle_decoder_next_vector_java_int(orcg_rle_decoder* dec, int32_t* vector, const uint8_t* is_null, uint64_t n,
                                           int is_repeating);
 const char* orcg_rle_decoder_last_error(const orcg_rle_decoder* dec);
+/* A decoder with Java's rules: new RunLengthIntegerReaderV2(input, signed,
+ * skipCorrupt) (java/core/src/java/org/apache/orc/impl/
+ * RunLengthIntegerReaderV2.java:47-52), for the Java faces above. Where the
+ * Java reader differs from the C++ one (it checks less):
+ *  - a DELTA run with a bit width and one value (length byte 0) is not an
+ *    error: Java emits the first value and first + deltaBase (:125-145);
+ *  - PATCHED_BASE with pw + pgw > 64 fails with Java's IOException text
+ *    ("Corruption in ORC data encountered. To skip reading corrupted data,
+ *    set hive.exec.orc.skip.corrupt.data to true", ORCG_PARSE_ERROR) unless
+ *    skip_corrupt, which decodes it reading the patch list at
+ *    getClosestFixedBits(pw + pgw) bits an entry with Java's shift semantics
+ *    (:196-260: pw = 64 leaves no patch bits, so the values are base + the
+ *    packed literals);
+ *  - PATCHED_BASE with pl == 0 fails as Java's unpackedPatch[0] does
+ *    (ArrayIndexOutOfBoundsException "Index 0 out of bounds for length 0",
+ *    ORCG_PARSE_ERROR), after the run's bytes are read.
+ * Truncated runs keep the C++ reader's "bad read" errors (Java's InStream
+ * returns -1 bytes there instead of failing). Decoded by the wave-walk
+ * kernel (ORCG_RLEV2_WAVE_WALK). */
+int orcg_rle_decoder_create_java(orcg_ctx* ctx, const uint8_t* src, uint64_t src_len, int is_signed,
+                                 int skip_corrupt, orcg_rle_decoder** out);
 
 /* ---- byte RLE / boolean RLE (PRESENT, BOOLEAN, BYTE streams) -------------
  * Replaces ByteRleDecoderImpl / BooleanRleDecoderImpl (c++/src/ByteRLE.hh:

@@ -17,6 +17,7 @@ from .rle import (  # noqa: F401
     byterle_decode_device,
     create_boolean_rle_decoder,
     create_byte_rle_decoder,
+    create_java_rle_decoder,
     create_rle_decoder,
     decimal_decode_device,
     decode_integer_column,

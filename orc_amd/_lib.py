@@ -69,6 +69,7 @@ SIGNATURES = [
     ("orcg_rlev2_decode_i32", [vp, vp, u64, i32, vp, u64, vp], i32),
     ("orcg_rlev2_decode_i16", [vp, vp, u64, i32, vp, u64, vp], i32),
     ("orcg_rle_decoder_create", [vp, vp, u64, i32, i32, ctypes.POINTER(vp)], i32),
+    ("orcg_rle_decoder_create_java", [vp, vp, u64, i32, i32, ctypes.POINTER(vp)], i32),
     ("orcg_rle_decoder_destroy", [vp], None),
     ("orcg_rle_decoder_next_i64", [vp, vp, u64, vp], i32),
     ("orcg_rle_decoder_next_i32", [vp, vp, u64, vp], i32),

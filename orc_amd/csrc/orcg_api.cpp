@@ -30,6 +30,10 @@ const char* dev_error_message(uint32_t code) {
     case kErrV1BadRead: return "bad read in readByte";
     case kErrDecimalScale: return "Decimal scale out of range";
     case kErrHive11Overflow: return "Hive 0.11 decimal was more than 38 digits.";
+    case kErrJavaCorrupt:
+      return "Corruption in ORC data encountered. To skip reading corrupted data, set "
+             "hive.exec.orc.skip.corrupt.data to true";
+    case kErrJavaPatchIndex: return "Index 0 out of bounds for length 0";
   }
   return "unknown device error";
 }
@@ -93,7 +97,7 @@ uint32_t closest_fixed_bits(uint32_t n) {
 // Parses the run at `pos`. Returns kErrNone and sets run_len (values) and
 // run_end (bytes), or a DevErr.
 uint32_t parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_len,
-                   uint64_t* run_end) {
+                   uint64_t* run_end, int java = 0) {
   const uint32_t fb = s[pos];
   const uint32_t kind = fb >> 6;
   if (kind == 0) {
@@ -103,7 +107,7 @@ uint32_t parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_l
     return *run_end > len ? kErrBadRead : kErrNone;
   }
   if (pos + 2 > len) return kErrBadRead;
-  const uint64_t L = ((uint64_t)(fb & 1) << 8 | s[pos + 1]) + 1;
+  uint64_t L = ((uint64_t)(fb & 1) << 8 | s[pos + 1]) + 1;
   *run_len = L;
   if (kind == 1 || kind == 2) {
     const uint32_t W = kFbs[(fb >> 1) & 0x1f];
@@ -116,15 +120,18 @@ uint32_t parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_l
       const uint32_t pbs = kFbs[third & 0x1f];
       const uint32_t pgw = (fourth >> 5) + 1;
       pl = fourth & 0x1f;
-      if (pl == 0) return kErrPatchedPl0;
+      if (pl == 0 && !java) return kErrPatchedPl0;
       if (pos + 4 + bw > len) return kErrBadRead;
       data = pos + 4 + bw;
       if (data + (W * L + 7) / 8 > len) return kErrBadRead;
-      if (pbs + pgw > 64) return kErrPatchedWidth;
+      // Java (RunLengthIntegerReaderV2.java:196-202): with skipCorrupt the
+      // list is read at getClosestFixedBits(pw + pgw) bits an entry
+      if (pbs + pgw > 64 && java != 2) return java ? kErrJavaCorrupt : kErrPatchedWidth;
       cfb = closest_fixed_bits(pbs + pgw);
     }
     *run_end = data + (W * L + 7) / 8 + ((uint64_t)cfb * pl + 7) / 8;
-    return *run_end > len ? kErrBadRead : kErrNone;
+    if (*run_end > len) return kErrBadRead;
+    return kind == 2 && pl == 0 ? kErrJavaPatchIndex : kErrNone;  // Java: unpackedPatch[0] of an empty list
   }
   const uint32_t fbo = (fb >> 1) & 0x1f;
   const uint32_t W = fbo ? kFbs[fbo] : 0;
@@ -136,7 +143,10 @@ uint32_t parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_l
       b = s[q++];
     } while (b >= 0x80);
   }
-  if (W != 0 && L < 2) return kErrDeltaLength;
+  if (W != 0 && L < 2) {
+    if (!java) return kErrDeltaLength;
+    *run_len = L = 2;  // Java (:125-145): the first value, first + deltaBase, no deltas
+  }
   *run_end = q + (W ? ((uint64_t)W * (L - 2) + 7) / 8 : 0);
   return *run_end > len ? kErrBadRead : kErrNone;
 }
@@ -262,14 +272,14 @@ uint32_t host_parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* 
 }  // namespace orcg
 
 orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes,
-                                  uint64_t max_values) {
+                                  uint64_t max_values, int java) {
   auto* p = new orcg_rlev2_plan();
   uint64_t pos = 0, vi = 0;
   uint64_t seg_b = 0, seg_v = 0;
   bool open = false;
   while (pos < len) {
     uint64_t L = 0, end = 0;
-    const uint32_t e = parse_run(src, len, pos, &L, &end);
+    const uint32_t e = parse_run(src, len, pos, &L, &end, java);
     if (e != kErrNone) {
       p->err = e;
       p->err_at = vi;
@@ -508,7 +518,7 @@ int orcg_rlev2_decode_positions_device(orcg_ctx* c, const uint8_t* d_src, uint64
 // ---- host-buffer decode ----------------------------------------------------
 // Decodes the first `count` values of a host stream into host `out` (dense).
 int decode_host_dense(Ctx* c, const uint8_t* src, uint64_t len, int is_signed,
-                             const orcg_rlev2_plan* plan, uint64_t count, void* out, int width) {
+                             const orcg_rlev2_plan* plan, uint64_t count, void* out, int width, int java) {
   if (count == 0) return ORCG_OK;
   hipSetDevice(c->device);
   void *d_src, *d_seg, *d_out;
@@ -522,7 +532,9 @@ int decode_host_dense(Ctx* c, const uint8_t* src, uint64_t len, int is_signed,
                                      hipMemcpyHostToDevice, c->stream),
                    "H2D segments");
   if (!rc)
-    rc = launch_rlev2(c, (const uint8_t*)d_src, len, is_signed, (const uint64_t*)d_seg,
+    rc = java ? launch_rlev2_decode(c, (const uint8_t*)d_src, len, is_signed, (const uint64_t*)d_seg,
+                                    plan->segs.size(), false, 0, 0, count, d_out, width, java)
+              : launch_rlev2(c, (const uint8_t*)d_src, len, is_signed, (const uint64_t*)d_seg,
                              plan->segs.size(), false, 0, 0, count, d_out, width);
   if (!rc)
     rc = hip_check(c, hipMemcpyAsync(out, d_out, count * (size_t)width, hipMemcpyDeviceToHost, c->stream),
@@ -574,6 +586,7 @@ int orcg_rlev2_decode_i16(orcg_ctx* c, const uint8_t* s, uint64_t l, int sg, con
 struct orcg_rle_decoder {
   Ctx* ctx = nullptr;
   int is_signed = 0;
+  int java = 0;  // Java's RunLengthIntegerReaderV2 rules (launch_rlev2_decode `java`)
   std::vector<uint8_t> src;
   std::unique_ptr<orcg_rlev2_plan> plan;
   uint64_t origin = 0;          // byte offset the decoded values start at
@@ -591,9 +604,9 @@ struct orcg_rle_decoder {
     cursor = 0;
     const uint8_t* s = src.data() + from;
     const uint64_t len = src.size() - from;
-    plan.reset(make_plan(s, len, 16u << 10, 8192));
+    plan.reset(make_plan(s, len, 16u << 10, 8192, java));
     values.assign(plan->values, 0);
-    int rc = decode_host_dense(ctx, s, len, is_signed, plan.get(), plan->values, values.data(), 8);
+    int rc = decode_host_dense(ctx, s, len, is_signed, plan.get(), plan->values, values.data(), 8, java);
     if (rc) return fail(rc, ctx->last_error);
     return ORCG_OK;
   }
@@ -638,6 +651,27 @@ int orcg_rle_decoder_create(orcg_ctx* c, const uint8_t* src, uint64_t len, int i
   auto* d = new orcg_rle_decoder();
   d->ctx = c;
   d->is_signed = is_signed;
+  d->src.assign(src, src + len);
+  int rc = d->load_from(0);
+  if (rc) {
+    c->last_error = d->last_error;
+    delete d;
+    return rc;
+  }
+  *out = d;
+  return ORCG_OK;
+}
+
+// new RunLengthIntegerReaderV2(input, signed, skipCorrupt)
+// (java/core/src/java/org/apache/orc/impl/RunLengthIntegerReaderV2.java:47-52)
+int orcg_rle_decoder_create_java(orcg_ctx* c, const uint8_t* src, uint64_t len, int is_signed, int skip_corrupt,
+                                 orcg_rle_decoder** out) {
+  if (!c || !out || (len && !src)) return ORCG_INVALID_ARGUMENT;
+  *out = nullptr;
+  auto* d = new orcg_rle_decoder();
+  d->ctx = c;
+  d->is_signed = is_signed;
+  d->java = skip_corrupt ? 2 : 1;
   d->src.assign(src, src + len);
   int rc = d->load_from(0);
   if (rc) {

@@ -26,6 +26,9 @@ enum DevErr : uint32_t {
   kErrV1BadRead = 8,       // "bad read in readByte" (RLEv1.cc:141-146)
   kErrDecimalScale = 9,    // "Decimal scale out of range" (ColumnReader.cc:1348)
   kErrHive11Overflow = 10, // "Hive 0.11 decimal was more than 38 digits." (ColumnReader.cc:1654)
+  // Java face (RunLengthIntegerReaderV2.java, readPatchedBaseValues :149-260)
+  kErrJavaCorrupt = 11,    // IOException "Corruption in ORC data encountered. ..." (pw + pgw > 64, :196-200)
+  kErrJavaPatchIndex = 12, // ArrayIndexOutOfBoundsException: pl == 0 reads unpackedPatch[0] (:207)
 };
 
 const char* dev_error_message(uint32_t code);
@@ -151,10 +154,14 @@ int sync_ctx(Ctx* ctx);
 
 // Kernel launchers (rlev2_kernels.hip). segtab is either orcg_segment[] or the
 // row-index positions array (positions_mode, with rows_per_group).
+// java: 0 = the C++ reader's rules; 1 = Java's RunLengthIntegerReaderV2
+// (DELTA runs of one value with a bit width decode two values, PATCHED_BASE
+// with pl == 0 fails as Java's array index, pw + pgw > 64 fails with Java's
+// IOException); 2 = Java with skipCorrupt (pw + pgw > 64 decodes, :196-202).
 int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                         uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
-                        void* d_dst, int dst_bytes);
+                        void* d_dst, int dst_bytes, int java = 0);
 
 // Dense -> row placement fused into a decode (out non-null; ColumnReader's
 // null skipping, c++/src/ColumnReader.cc:81-104, RleDecoderV2.cc:437-453):
@@ -361,7 +368,7 @@ struct orcg_rlev2_plan {
   uint64_t err_at = 0;
 };
 
-orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
+orcg_rlev2_plan* make_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values, int java = 0);
 namespace orcg {
 // The RLEv2 run at `pos` (host): kErrNone with its value count and end, or a DevErr.
 uint32_t host_parse_run(const uint8_t* s, uint64_t len, uint64_t pos, uint64_t* run_len, uint64_t* run_end);
@@ -370,4 +377,4 @@ orcg_rlev2_plan* make_v1_plan(const uint8_t* src, uint64_t len, uint64_t max_byt
 orcg_rlev2_plan* make_byte_plan(const uint8_t* src, uint64_t len, uint64_t max_bytes, uint64_t max_values);
 // H2D + RLEv2 decode of the first `count` values + D2H into host `out`.
 int decode_host_dense(orcg::Ctx* c, const uint8_t* src, uint64_t len, int is_signed,
-                      const orcg_rlev2_plan* plan, uint64_t count, void* out, int width);
+                      const orcg_rlev2_plan* plan, uint64_t count, void* out, int width, int java = 0);

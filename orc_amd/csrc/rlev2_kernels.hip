@@ -103,7 +103,16 @@ struct Window {
   }
 };
 
-template <typename T, bool kPositions>
+// kJava: 0 = the C++ reader's rules; 1 = Java's RunLengthIntegerReaderV2
+// (java/core/src/java/org/apache/orc/impl/RunLengthIntegerReaderV2.java):
+// readDeltaValues (:86-147) never rejects a one-value DELTA run with a bit
+// width (it emits the first value and first + deltaBase: two values, no
+// packed deltas); readPatchedBaseValues (:149-260) reads an empty patch list
+// and fails on unpackedPatch[0] (after the run's bytes), and fails on pw +
+// pgw > 64 with its IOException; 2 = Java with skipCorrupt, which reads such
+// a list at getClosestFixedBits(pw + pgw) bits an entry with Java's shifts
+// (by the width mod 64: pw = 64 gives gap = the entry, patch = 0).
+template <typename T, bool kPositions, int kJava>
 __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
     const uint8_t* __restrict__ src, uint64_t src_len, int is_signed,
     const uint64_t* __restrict__ segtab, uint64_t nsegs, uint64_t rows_per_group,
@@ -185,19 +194,23 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
         pbs = fbs_width(third & 0x1fu);
         const uint32_t pgw = (fourth >> 5) + 1u;
         pl = fourth & 0x1fu;
-        if (pl == 0) { report(err, vi, kErrPatchedPl0); return; }
+        if (pl == 0 && kJava == 0) { report(err, vi, kErrPatchedPl0); return; }
         if (pos + 4 + bw > src_len) { report(err, vi, kErrBadRead); return; }
         for (uint32_t i = 0; i < bw; ++i) base = (base << 8) | win.byte(rel + 4 + i);
         const uint64_t m = 1ull << (bw * 8 - 1);
         if (base & m) base = 0 - (base & ~m);  // sign-magnitude (:311-317)
         data = pos + 4 + bw;
         if (data + ((uint64_t)W * L + 7) / 8 > src_len) { report(err, vi, kErrBadRead); return; }
-        if (pbs + pgw > 64) { report(err, vi, kErrPatchedWidth); return; }
+        if (pbs + pgw > 64 && kJava != 2) {
+          report(err, vi, kJava ? kErrJavaCorrupt : kErrPatchedWidth);
+          return;
+        }
         cfb = closest_fixed_bits(pbs + pgw);
       }
       const uint64_t data_end = data + ((uint64_t)W * L + 7) / 8;
       run_end = data_end + ((uint64_t)cfb * pl + 7) / 8;
       if (run_end > src_len) { report(err, vi, kErrBadRead); return; }
+      if (kJava && kind == 2 && pl == 0) { report(err, vi, kErrJavaPatchIndex); return; }
       if (run_end > seg_end) { report(err, vi, kErrBadSegment); return; }
 
       if (vi + L > value_begin && vi < value_end) {
@@ -223,7 +236,10 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
             const uint32_t bit = (uint32_t)lane * cfb;
             entry = field(load12(rs, prel + (bit >> 3)), prel + (bit >> 3), bit & 7u, cfb);
           }
-          const uint64_t pmask = (1ull << pbs) - 1;  // pbs <= 63 here
+          // pbs <= 63 here, except under skipCorrupt: Java shifts by the
+          // width mod 64 (pw = 64: no patch bits, the whole entry is the gap)
+          const uint32_t psh = pbs & 63u;
+          const uint64_t pmask = (1ull << psh) - 1;
           const uint32_t e_lo = (uint32_t)entry, e_hi = (uint32_t)(entry >> 32);
           if (!patch_lds_clean) {
 #pragma unroll
@@ -236,7 +252,7 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
             bool first = true;
             for (uint32_t k = 0; k < pl; ++k) {
               const uint64_t e = ((uint64_t)rdlane(e_hi, k) << 32) | rdlane(e_lo, k);
-              const uint64_t gp = e >> pbs, pv = e & pmask;
+              const uint64_t gp = e >> psh, pv = e & pmask;
               cum += gp;
               if (gp == 255 && pv == 0) continue;
               if ((!first && cum == prev) || cum >= L) break;
@@ -307,7 +323,10 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
       }
       const uint64_t first = is_signed ? unzigzag(vals[0]) : vals[0];
       const uint64_t dbase = unzigzag(vals[1]);
-      if (W != 0 && L < 2) { report(err, vi, kErrDeltaLength); return; }
+      if (W != 0 && L < 2) {
+        if (kJava == 0) { report(err, vi, kErrDeltaLength); return; }
+        L = 2;  // Java: the first value and first + deltaBase (:125-145)
+      }
       const uint64_t data = q;
       run_end = data + (W ? ((uint64_t)W * (L - 2) + 7) / 8 : 0);
       if (run_end > src_len) { report(err, vi, kErrBadRead); return; }
@@ -370,16 +389,23 @@ __global__ __launch_bounds__(kWave) void rlev2_decode_kernel(
 int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                         uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
-                        void* d_dst, int dst_bytes) {
+                        void* d_dst, int dst_bytes, int java) {
   if (nsegs == 0 || nvalues == 0) return ORCG_OK;
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   if (src_len >= (1ull << 56)) return set_error(ctx, ORCG_INVALID_ARGUMENT, "stream too long");
+  if (java && positions_mode) return set_error(ctx, ORCG_INVALID_ARGUMENT, "Java rules take segment tables");
   const dim3 grid((unsigned)nsegs), block(kWave);
   const int sg = is_signed ? 1 : 0;
-#define ORCG_LAUNCH(T, P)                                                                      \
-  hipLaunchKernelGGL((rlev2_decode_kernel<T, P>), grid, block, 0, ctx->stream, d_src, src_len, \
-                     sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst,     \
+#define ORCG_LAUNCH1(T, P, J)                                                                     \
+  hipLaunchKernelGGL((rlev2_decode_kernel<T, P, J>), grid, block, 0, ctx->stream, d_src, src_len, \
+                     sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst,        \
                      ctx->d_err)
+#define ORCG_LAUNCH(T, P)                                  \
+  do {                                                     \
+    if (java == 2) ORCG_LAUNCH1(T, false, 2);              \
+    else if (java == 1) ORCG_LAUNCH1(T, false, 1);         \
+    else ORCG_LAUNCH1(T, P, 0);                            \
+  } while (0)
   switch (dst_bytes) {
     case 8:
       if (positions_mode) ORCG_LAUNCH(int64_t, true); else ORCG_LAUNCH(int64_t, false);
@@ -394,6 +420,7 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
       return set_error(ctx, ORCG_INVALID_ARGUMENT, "dst_bytes must be 8, 4 or 2");
   }
 #undef ORCG_LAUNCH
+#undef ORCG_LAUNCH1
   return hip_check(ctx, hipGetLastError(), "rlev2_decode_kernel launch");
 }
 

@@ -109,13 +109,20 @@ class RleDecoderV2:
     memory: the whole stream is decoded on the GPU at construction and
     next()/skip()/seek() serve it with the reference's run-state semantics."""
 
-    def __init__(self, data, is_signed, ctx=None, version=RleVersion_2):
+    def __init__(self, data, is_signed, ctx=None, version=RleVersion_2, java=None):
+        """java=None: the C++ reader's rules; java=False / True: Java's
+        RunLengthIntegerReaderV2 with skipCorrupt off / on
+        (orcg_rle_decoder_create_java)."""
         self._L = _lib.load()
         self.ctx = ctx or default_context()
         self._buf = np.frombuffer(bytes(data), dtype=np.uint8).copy()
         h = ctypes.c_void_p()
-        rc = self._L.orcg_rle_decoder_create(self.ctx.handle, _ptr(self._buf), self._buf.size,
-                                            int(bool(is_signed)), version, ctypes.byref(h))
+        if java is None:
+            rc = self._L.orcg_rle_decoder_create(self.ctx.handle, _ptr(self._buf), self._buf.size,
+                                                int(bool(is_signed)), version, ctypes.byref(h))
+        else:
+            rc = self._L.orcg_rle_decoder_create_java(self.ctx.handle, _ptr(self._buf), self._buf.size,
+                                                     int(bool(is_signed)), int(bool(java)), ctypes.byref(h))
         check(rc, self.ctx.last_error)
         self._h = h
 
@@ -183,6 +190,13 @@ def rlev2_variants():
     out = (ctypes.c_int * max(n, 1))()
     L.orcg_rlev2_variants(out, n)
     return list(out[:n])
+
+
+def create_java_rle_decoder(data, is_signed, skip_corrupt=False, ctx=None):
+    """new RunLengthIntegerReaderV2(input, signed, skipCorrupt)
+    (java/core/src/java/org/apache/orc/impl/RunLengthIntegerReaderV2.java:47-52)
+    over the GPU decode: the Java face's decoder, with Java's checks."""
+    return RleDecoderV2(data, is_signed, ctx=ctx, java=bool(skip_corrupt))
 
 
 def create_rle_decoder(data, is_signed, version=RleVersion_2, ctx=None):

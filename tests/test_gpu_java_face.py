@@ -166,3 +166,197 @@ def test_is_repeating_on_repeated_runs():
     assert rep and list(v) == [1, 1, 1]
     v, rep = dec.next_vector_java(2)
     assert rep and list(v) == [7, 7]
+
+
+# ---- Java's corrupt-data rules (orcg_rle_decoder_create_java) --------------
+# The runs below are hand-built; the expected values are restated from
+# RunLengthIntegerReaderV2.java (readDeltaValues :86-147,
+# readPatchedBaseValues :149-260) by java_run() with Java's long semantics
+# (64-bit two's complement, shifts by the count mod 64).
+
+def _java_widths(code):
+    return code + 1 if code < 24 else [26, 28, 30, 32, 40, 48, 56, 64][code - 24]
+
+
+def _java_closest(n):
+    if n == 0:
+        return 1
+    for w in (24, 26, 28, 30, 32, 40, 48, 56):
+        if n <= w:
+            return n if w == 24 else w
+    return 64
+
+
+def _s64(x):
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >> 63 else x
+
+
+def _read_ints(buf, p, n, bits):
+    """SerializationUtils.readInts: n big-endian `bits`-bit fields from byte p."""
+    out, acc, have = [], 0, 0
+    for _ in range(max(n, 0)):
+        while have < bits:
+            acc = (acc << 8) | buf[p]
+            p += 1
+            have += 8
+        out.append((acc >> (have - bits)) & ((1 << bits) - 1))
+        have -= bits
+        acc &= (1 << have) - 1
+    return out, p
+
+
+def _varint(buf, p):
+    v, sh = 0, 0
+    while True:
+        b = buf[p]
+        p += 1
+        v |= (b & 0x7F) << sh
+        sh += 7
+        if b < 0x80:
+            return v, p
+
+
+def java_run(buf, p, signed, skip_corrupt):
+    """One run of RunLengthIntegerReaderV2.readValues: (values, next byte) or
+    raises ValueError with the Java exception's message."""
+    fb = buf[p]
+    kind = fb >> 6
+    if kind == 0:  # readShortRepeatValues
+        size, n = ((fb >> 3) & 7) + 1, (fb & 7) + 3
+        v = int.from_bytes(bytes(buf[p + 1:p + 1 + size]), "big")
+        if signed:
+            v = (v >> 1) ^ -(v & 1)
+        return [v] * n, p + 1 + size
+    if kind == 3:  # readDeltaValues
+        fbw = (fb >> 1) & 0x1F
+        fbw = _java_widths(fbw) if fbw else 0
+        ln = ((fb & 1) << 8) | buf[p + 1]  # no + 1 in Java
+        first, q = _varint(buf, p + 2)
+        if signed:
+            first = (first >> 1) ^ -(first & 1)
+        out = [first]
+        db, q = _varint(buf, q)
+        db = (db >> 1) ^ -(db & 1)
+        if fbw == 0:
+            out += [first + db * (k + 1) for k in range(ln)]
+            return [_s64(x) for x in out], q
+        out.append(first + db)
+        ln -= 1
+        ds, q = _read_ints(buf, q, ln, fbw)
+        for d in ds:
+            out.append(out[-1] - d if db < 0 else out[-1] + d)
+        return [_s64(x) for x in out], q
+    assert kind == 2, "test runs are SHORT_REPEAT / DELTA / PATCHED_BASE"
+    fbw = _java_widths((fb >> 1) & 0x1F)
+    ln = (((fb & 1) << 8) | buf[p + 1]) + 1
+    third, fourth = buf[p + 2], buf[p + 3]
+    bw, pw = ((third >> 5) & 7) + 1, _java_widths(third & 0x1F)
+    pgw, pl = ((fourth >> 5) & 7) + 1, fourth & 0x1F
+    base = int.from_bytes(bytes(buf[p + 4:p + 4 + bw]), "big")
+    mask = 1 << (bw * 8 - 1)
+    if base & mask:
+        base = -(base & ~mask)
+    unpacked, q = _read_ints(buf, p + 4 + bw, ln, fbw)
+    if pw + pgw > 64 and not skip_corrupt:
+        raise ValueError("Corruption in ORC data encountered. To skip reading corrupted data, "
+                         "set hive.exec.orc.skip.corrupt.data to true")
+    patches, q = _read_ints(buf, q, pl, _java_closest(pw + pgw))
+    if pl == 0:
+        raise ValueError("Index 0 out of bounds for length 0")
+    pmask = ((1 << (pw & 63)) - 1) & ((1 << 64) - 1)  # (1L << pw) - 1
+
+    def gp(k):
+        return patches[k] >> (pw & 63), patches[k] & pmask
+
+    idx = 0
+    gap, patch = gp(0)
+    actual = 0
+    while gap == 255 and patch == 0:
+        actual += 255
+        idx += 1
+        gap, patch = gp(idx)
+    actual += gap
+    out = []
+    for i in range(ln):
+        if i == actual:
+            out.append(base + (unpacked[i] | ((patch << (fbw & 63)) & ((1 << 64) - 1))))
+            idx += 1
+            if idx < pl:
+                gap, patch = gp(idx)
+                actual = 0
+                while gap == 255 and patch == 0:
+                    actual += 255
+                    idx += 1
+                    gap, patch = gp(idx)
+                actual += gap + i
+        else:
+            out.append(base + unpacked[i])
+    return [_s64(x) for x in out], q
+
+
+def java_stream(buf, signed, skip_corrupt):
+    out, p = [], 0
+    while p < len(buf):
+        v, p = java_run(buf, p, signed, skip_corrupt)
+        out += v
+    return out
+
+
+SR5 = bytes([0x00, 0x0A])  # SHORT_REPEAT: 3 x 5 (signed)
+# PATCHED_BASE, W = 8, 4 values, base 5, pw = 64 (code 31), pgw = 2, pl = 2:
+# pw + pgw > 64; entries 3 and 1000 (64 bits each: getClosestFixedBits(66))
+PATCHED_PW64 = (bytes([0x80 | (7 << 1), 3, (0 << 5) | 31, (1 << 5) | 2, 0x05, 1, 2, 3, 4]) +
+                (3).to_bytes(8, "big") + (1000).to_bytes(8, "big"))
+# PATCHED_BASE with pl == 0 (pw = 4, pgw = 1): no patch bytes
+PATCHED_PL0 = bytes([0x80 | (7 << 1), 3, (0 << 5) | 3, (0 << 5) | 0, 0x05, 1, 2, 3, 4])
+# DELTA, W = 4, length byte 0 (C++: one value, an error), first 100, step -7
+DELTA_LEN0 = bytes([0xC0 | (3 << 1), 0x00, 0xC8, 0x01, 0x0D])
+
+JAVA_CASES = [
+    ("patched_pw64", PATCHED_PW64 + SR5, "Corrupt PATCHED_BASE encoded data \\(patchBitSize \\+ pgw > 64\\)!"),
+    ("patched_pl0", PATCHED_PL0 + SR5, "Corrupt PATCHED_BASE encoded data \\(pl==0\\)!"),
+    ("delta_len0", DELTA_LEN0 + SR5, "Illegal run length for delta encoding"),
+]
+
+
+@pytest.mark.parametrize("name,data,cxx_msg", JAVA_CASES, ids=[c[0] for c in JAVA_CASES])
+@pytest.mark.parametrize("skip_corrupt", [False, True])
+def test_java_corrupt_data_rules(name, data, cxx_msg, skip_corrupt):
+    """Java's RunLengthIntegerReaderV2 checks less than RleDecoderV2: with
+    skipCorrupt a PATCHED_BASE run with pw + pgw > 64 decodes (otherwise
+    Java's IOException text), pl == 0 fails as Java's array index, and a
+    one-value DELTA run with a bit width yields two values. The C++-rules
+    decoder keeps the reference's ParseErrors on the same bytes."""
+    import orc_amd
+
+    try:
+        want, err = java_stream(data, True, skip_corrupt), None
+    except ValueError as e:
+        want, err = None, str(e)
+    dec = orc_amd.create_java_rle_decoder(data, True, skip_corrupt=skip_corrupt)
+    if err is None:
+        got, rep = dec.next_vector_java(len(want))
+        assert [int(x) for x in got] == want
+        with pytest.raises(orc_amd.ParseError):
+            dec.next_vector_java(1)  # past the stream
+    else:
+        with pytest.raises(orc_amd.ParseError, match=err.replace("(", "\\(").replace(")", "\\)")):
+            dec.next_vector_java(4)
+    cxx = orc_amd.create_rle_decoder(data, True)
+    with pytest.raises(orc_amd.ParseError, match=cxx_msg):
+        cxx.next(4)
+
+
+def test_java_rules_match_cxx_on_good_streams():
+    """On the reference's KAT streams (all well-formed) the Java-rules decoder
+    gives the C++ decoder's values."""
+    import orc_amd
+
+    for fx in RLEV2:
+        data = bytes.fromhex(fx["data"])
+        n = sum(1 for e in fx["expected"] if e is not None) if fx.get("not_null") is None else \
+            sum(1 for m in fx["not_null"] if m)
+        a = orc_amd.create_rle_decoder(data, fx["signed"]).next(n)
+        b = orc_amd.create_java_rle_decoder(data, fx["signed"], skip_corrupt=True).next(n)
+        np.testing.assert_array_equal(a, b, err_msg=fx["name"])
