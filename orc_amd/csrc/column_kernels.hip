@@ -111,6 +111,16 @@ __device__ uint64_t lb_lookback(unsigned long long* status, uint32_t t, uint32_t
   return excl;
 }
 
+// StringDirectColumnReader::computeSize's checks (ColumnReader.cc:694-710),
+// fused into the scan of the lengths: flags[0] |= 1 if a length is negative,
+// flags[1] |= 1 if the running total wraps (a start plus its length below
+// the start: with non-negative lengths, the size_t total overflowed). The
+// flags are zero before the scan (the reader's read-back block).
+__device__ __forceinline__ void strlen_flags(unsigned long long* flags, bool neg, bool wrap) {
+  if (__any(neg) && (threadIdx.x % kWave) == 0) atomicOr(flags, 1ull);
+  if (__any(wrap) && (threadIdx.x % kWave) == 0) atomicOr(flags + 1, 1ull);
+}
+
 __global__ __launch_bounds__(kThreads) void tile_count_kernel(const uint8_t* __restrict__ nn, uint64_t n,
                                                                uint32_t* __restrict__ counts) {
   __shared__ uint32_t red[kThreads / kWave];
@@ -361,40 +371,25 @@ __global__ __launch_bounds__(kThreads) void dict_multi_kernel(const DictJob* __r
   (void)njobs;
 }
 
-// Multi-workgroup exclusive scan of int64 values (lengths -> offsets):
-// per-tile sums, one-workgroup scan of the sums, per-tile scan. Used for
-// direct string lengths (DATA offsets, StringDirectColumnReader::next,
-// c++/src/ColumnReader.cc:725-793) and list/map lengths (ListColumnReader::
-// nextInternal, :960-993) where the value count is the stripe's row count.
+// Exclusive scans of int64 values (lengths -> offsets): direct string
+// lengths (DATA offsets, StringDirectColumnReader::next, c++/src/
+// ColumnReader.cc:725-793) and list/map lengths (ListColumnReader::
+// nextInternal, :960-993), one workgroup below 8,192 values, else the
+// single-pass look-back kernel over 4,096-value tiles.
 constexpr int kScanTile = 4096;  // 256 threads x 16 values
 
-__global__ __launch_bounds__(kThreads) void tile_sum_kernel(const int64_t* __restrict__ in, uint64_t n,
-                                                             uint64_t* __restrict__ sums) {
-  __shared__ uint64_t red[kThreads / kWave];
-  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16u;
-  uint64_t s = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k)
-    if (i0 + k < n) s += (uint64_t)in[i0 + k];
-  s = wave_inclusive_scan(s);
-  const int lane = threadIdx.x % kWave;
-  if (lane == kWave - 1) red[threadIdx.x / kWave] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (int w = 0; w < kThreads / kWave; ++w) t += red[w];
-    sums[blockIdx.x] = t;
-  }
-}
-
 // Exclusive scan of `n` uint64 into `offsets` (n + 1 entries), one workgroup.
+// (flags, may be null: strlen_flags below)
 __global__ __launch_bounds__(1024) void scan64_kernel(const uint64_t* __restrict__ in, uint64_t n,
-                                                       uint64_t* __restrict__ offsets) {
+                                                       uint64_t* __restrict__ offsets,
+                                                       unsigned long long* __restrict__ flags = nullptr,
+                                                       uint64_t* __restrict__ total = nullptr) {
   __shared__ uint64_t wsum[1024 / kWave];
   __shared__ uint64_t carry_s;
   const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
   if (threadIdx.x == 0) carry_s = 0;
   __syncthreads();
+  bool neg = false, wrap = false;
   for (uint64_t b = 0; b < n; b += 1024) {
     const uint64_t i = b + threadIdx.x;
     const uint64_t x = i < n ? in[i] : 0;
@@ -403,38 +398,19 @@ __global__ __launch_bounds__(1024) void scan64_kernel(const uint64_t* __restrict
     __syncthreads();
     uint64_t before = carry_s;
     for (int w = 0; w < wv; ++w) before += wsum[w];
-    if (i < n) offsets[i] = before + inc - x;
+    const uint64_t st = before + inc - x;
+    if (i < n) offsets[i] = st;
+    neg |= i < n && (int64_t)x < 0;
+    wrap |= i < n && st + x < st;
     __syncthreads();
     if (threadIdx.x == 1023) carry_s = before + inc;
     __syncthreads();
   }
-  if (threadIdx.x == 0) offsets[n] = carry_s;
-}
-
-__global__ __launch_bounds__(kThreads) void tile_scan_kernel(const int64_t* __restrict__ in, uint64_t n,
-                                                              const uint64_t* __restrict__ tile_off,
-                                                              int64_t* __restrict__ out) {
-  __shared__ uint64_t wsum[kThreads / kWave];
-  const int lane = threadIdx.x % kWave, wv = threadIdx.x / kWave;
-  const uint64_t i0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * 16u;
-  int64_t v[16];
-  uint64_t s = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    v[k] = i0 + k < n ? in[i0 + k] : 0;
-    s += (uint64_t)v[k];
+  if (threadIdx.x == 0) {
+    offsets[n] = carry_s;
+    if (total) *total = carry_s;
   }
-  const uint64_t inc = wave_inclusive_scan(s);
-  if (lane == kWave - 1) wsum[wv] = inc;
-  __syncthreads();
-  uint64_t run = tile_off[blockIdx.x] + inc - s;
-  for (int w = 0; w < wv; ++w) run += wsum[w];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    if (i0 + k < n) out[i0 + k] = (int64_t)run;
-    run += (uint64_t)v[k];
-  }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = (int64_t)tile_off[gridDim.x];
+  if (flags) strlen_flags(flags, neg, wrap);
 }
 
 // Single-pass exclusive scan (decoupled look-back): workgroup tickets in
@@ -450,7 +426,9 @@ __global__ __launch_bounds__(kThreads) void tile_scan_kernel(const int64_t* __re
 __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const int64_t* __restrict__ in, uint64_t n,
                                                                  int64_t* __restrict__ out,
                                                                  unsigned long long* __restrict__ status,
-                                                                 uint32_t ntiles, uint32_t epoch) {
+                                                                 uint32_t ntiles, uint32_t epoch,
+                                                                 unsigned long long* __restrict__ flags,
+                                                                 uint64_t* __restrict__ total) {
   __shared__ uint64_t s_v[kScanTile + kScanTile / 16];  // one pad word per thread's 16 (bank spread)
   __shared__ uint64_t s_wsum[kThreads / kWave];
   __shared__ uint32_t s_tile;
@@ -496,11 +474,15 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const int64_t* 
   }
   __syncthreads();
   uint64_t run = s_excl + before;
+  bool neg = false, wrap = false;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     s_v[tid * 17 + k] = run;
+    neg |= (int64_t)v[k] < 0;
+    wrap |= run + v[k] < run;
     run += v[k];
   }
+  if (flags) strlen_flags(flags, neg, wrap);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -508,7 +490,10 @@ __global__ __launch_bounds__(kThreads) void scan_lookback_kernel(const int64_t* 
     const uint32_t e = (uint32_t)(k * kThreads + tid);
     if (i < n) out[i] = (int64_t)s_v[e + (e >> 4)];
   }
-  if (t == ntiles - 1 && tid == kThreads - 1) out[n] = (int64_t)(s_excl + agg);
+  if (t == ntiles - 1 && tid == kThreads - 1) {
+    out[n] = (int64_t)(s_excl + agg);
+    if (total) *total = s_excl + agg;
+  }
 }
 
 // Element conversions into the reference's batch types (LongVectorBatch /
@@ -528,22 +513,6 @@ __global__ void flag_negative_kernel(const int64_t* __restrict__ v, uint64_t n, 
   bool neg = false;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) neg |= v[i] < 0;
   if (__any(neg) && (threadIdx.x % kWave) == 0) atomicOr(flag, 1ull);
-}
-
-// StringDirectColumnReader::computeSize's checks (ColumnReader.cc:694-710)
-// over a column's lengths and their exclusive scan: flags[0] |= 1 if a length
-// is negative, flags[1] |= 1 if the running total wraps (a start below its
-// predecessor: with non-negative lengths, the size_t total overflowed).
-__global__ void strlen_check_kernel(const int64_t* __restrict__ len, const int64_t* __restrict__ start, uint64_t n,
-                                    unsigned long long* flags) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  bool neg = false, wrap = false;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    neg |= len[i] < 0;
-    wrap |= (uint64_t)start[i + 1] < (uint64_t)start[i];
-  }
-  if (__any(neg) && (threadIdx.x % kWave) == 0) atomicOr(flags, 1ull);
-  if (__any(wrap) && (threadIdx.x % kWave) == 0) atomicOr(flags + 1, 1ull);
 }
 
 // ---- row-index segmentation (ColumnReader::seekToRowGroup positions) ----
@@ -838,37 +807,28 @@ int launch_dict_multi(Ctx* ctx, const DictJob* jobs, uint32_t njobs) {
 
 namespace orcg {
 
-int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out) {
+int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out, uint64_t* d_flags,
+                          uint64_t* d_total) {
   if (n == 0) {
-    return hip_check(ctx, hipMemsetAsync(d_out, 0, sizeof(int64_t), ctx->stream), "scan memset");
+    int rc = hip_check(ctx, hipMemsetAsync(d_out, 0, sizeof(int64_t), ctx->stream), "scan memset");
+    if (!rc && d_total) rc = hip_check(ctx, hipMemsetAsync(d_total, 0, sizeof(uint64_t), ctx->stream), "scan memset");
+    return rc;
   }
+  unsigned long long* const fl = (unsigned long long*)d_flags;
   if (n <= 8192) {
-    // short inputs (varint tile counts, dictionary lengths): one workgroup,
-    // one launch instead of three
-    hipLaunchKernelGGL(scan64_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const uint64_t*)d_in, n, (uint64_t*)d_out);
+    // short inputs (varint tile counts, dictionary lengths): one workgroup
+    hipLaunchKernelGGL(scan64_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const uint64_t*)d_in, n, (uint64_t*)d_out,
+                       fl, d_total);
     return hip_check(ctx, hipGetLastError(), "scan launch");
   }
   const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
   if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many values");
-  static const bool three = getenv("ORCG_SCAN3") != nullptr;  // A/B: the three-launch scan
-  if (!three) {
-    unsigned long long* d_status;
-    uint32_t epoch;
-    const int rc = lb_status(ctx, kLbWords * (tiles + 1), &d_status, &epoch);
-    if (rc) return rc;
-    hipLaunchKernelGGL(scan_lookback_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n, d_out,
-                       d_status, (uint32_t)tiles, epoch);
-    return hip_check(ctx, hipGetLastError(), "scan launch");
-  }
-  void* d_sums;
-  int rc = scratch(ctx, 7, (2 * tiles + 1) * sizeof(uint64_t), &d_sums);
+  unsigned long long* d_status;
+  uint32_t epoch;
+  const int rc = lb_status(ctx, kLbWords * (tiles + 1), &d_status, &epoch);
   if (rc) return rc;
-  uint64_t* sums = (uint64_t*)d_sums;
-  uint64_t* toff = sums + tiles;
-  hipLaunchKernelGGL(tile_sum_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n, sums);
-  hipLaunchKernelGGL(scan64_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const uint64_t*)sums, tiles, toff);
-  hipLaunchKernelGGL(tile_scan_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n,
-                     (const uint64_t*)toff, d_out);
+  hipLaunchKernelGGL(scan_lookback_kernel, dim3((unsigned)tiles), dim3(kThreads), 0, ctx->stream, d_in, n, d_out,
+                     d_status, (uint32_t)tiles, epoch, fl, d_total);
   return hip_check(ctx, hipGetLastError(), "scan launch");
 }
 
@@ -896,15 +856,6 @@ int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_f
   hipLaunchKernelGGL(flag_negative_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_v, n,
                      (unsigned long long*)d_flag);
   return hip_check(ctx, hipGetLastError(), "flag launch");
-}
-
-int launch_strlen_check(Ctx* ctx, const int64_t* d_len, const int64_t* d_start, uint64_t n, uint64_t* d_flags) {
-  int rc = hip_check(ctx, hipMemsetAsync(d_flags, 0, 2 * sizeof(uint64_t), ctx->stream), "flag memset");
-  if (rc || n == 0) return rc;
-  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 1024);
-  hipLaunchKernelGGL(strlen_check_kernel, dim3(grid), dim3(256), 0, ctx->stream, d_len, d_start, n,
-                     (unsigned long long*)d_flags);
-  return hip_check(ctx, hipGetLastError(), "string length check launch");
 }
 
 // A small host -> device copy by the shader: the workgroups read the pinned,

@@ -192,7 +192,7 @@ struct RowScatter {
 // offset | its first value (segment-relative) << 32. Runs of passes the first
 // kernel expands itself (long runs, values past spg * slice) are not tabled.
 constexpr uint32_t kRtHdr = 6;
-constexpr uint32_t kSliceMax = 2048;
+constexpr uint32_t kSliceMax = 1024;
 struct RunTab {
   uint64_t* tab;
   uint32_t* hdr;
@@ -237,7 +237,8 @@ inline int stage_rle_jobs(Ctx* ctx, const RleJob* jobs, uint32_t n, const RleJob
 // table (stage_table in arena mode): plan_* group, order and stage the
 // jobs; run_multi enqueues the kernels (RLEv2 instances on side lanes).
 struct MultiLaunch {
-  int kind;           // 0 RLEv2 instance `variant`, 1 RLEv1, 2 dictionaries
+  int kind;           // 0 RLEv2 instance `variant`, 1 RLEv1, 2 dictionaries, 3 pinned single-stream RLEv2
+                      // (host job), 4 varint tile counts + scan (host VarintJob)
   int variant;
   const void* d_jobs;
   uint32_t njobs;
@@ -249,6 +250,16 @@ struct MultiLaunch {
   uint32_t spg = 0, slice = 0;
 };
 int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<MultiLaunch>& out);
+// A varint DATA stream's tile counts and their scan (the first value of each
+// kVarintTile-byte tile) ahead of its decode: the decimal columns' first two
+// launches, run before the batch's join (they need only the stream bytes).
+struct VarintJob {
+  const uint8_t* src;
+  uint64_t len;
+  int64_t* counts;
+  int64_t* base;    // ntiles + 1
+  uint64_t* total;  // the values in the stream (read-back slot)
+};
 int plan_rlev1_multi(Ctx* ctx, const V1SegDesc* segs, uint64_t nsegs, std::vector<MultiLaunch>& out);
 int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& launches);
 
@@ -329,12 +340,14 @@ int launch_union_offsets(Ctx* ctx, const uint8_t* d_tags, uint64_t n, uint32_t k
                          int64_t* d_offsets);
 
 // Multi-workgroup exclusive scan: d_out[0..n] (n + 1 entries). Scratch 7.
-int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out);
+// d_flags (may be null; zero on entry): StringDirect length checks fused into
+// the scan, [0] |= 1 for a negative input, [1] |= 1 when the total wraps.
+// d_total (may be null): the total (d_out[n]) also written there (e.g. a
+// slot of the reader's read-back block: no separate copy).
+int launch_exclusive_scan(Ctx* ctx, const int64_t* d_in, uint64_t n, int64_t* d_out, uint64_t* d_flags = nullptr,
+                          uint64_t* d_total = nullptr);
 // Number of non-zero bytes of d_nn[0..n) into *d_total (device). Scratch 5, 6.
 int launch_count_nonzero(Ctx* ctx, const uint8_t* d_nn, uint64_t n, uint64_t* d_total);
-// StringDirect lengths and their exclusive scan (n + 1 starts): d_flags[0] =
-// 1 if a length is negative, d_flags[1] = 1 if the total wrapped, else 0.
-int launch_strlen_check(Ctx* ctx, const int64_t* d_len, const int64_t* d_start, uint64_t n, uint64_t* d_flags);
 // *d_flag = 1 if any d_v[i] < 0, else 0.
 int launch_flag_negative(Ctx* ctx, const int64_t* d_v, uint64_t n, uint64_t* d_flag);
 enum WidenKind { kWidenI8 = 0, kWidenU8 = 1, kWidenF32 = 2 };

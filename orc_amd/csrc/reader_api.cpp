@@ -612,6 +612,11 @@ struct orcg_reader {
   };
   std::vector<DictJob> dict_batch;
   std::unordered_map<uint32_t, DictDone> dict_done;
+  // varint decimal DATA streams whose tile counts + scan run with the batch
+  // (before its join): their tile bases and value-count slots by column
+  std::deque<VarintJob> varint_jobs;
+  std::unordered_map<uint32_t, std::pair<int64_t*, const uint64_t*>> varint_pre;
+  int queue_varint(uint32_t id);
   std::vector<MultiLaunch> launches;
   std::unordered_map<uint64_t, std::pair<int64_t*, uint64_t>> batched;  // (column, slot) -> (values, count)
   int queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2);
@@ -706,8 +711,7 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
   const uint8_t* mask = slot == kSlotPresent ? cur_in_nn : cur_row_nn;
   const int64_t* prefix = cur_rows;
   int rc;
-  static const bool three = getenv("ORCG_SCAN3") != nullptr;  // A/B: count, scan and segtab launches
-  if (mask && !three) {
+  if (mask) {
     // the row groups' set-row prefix and the segment table in one launch
     ORCG_ALLOC(int64_t, pre, G + 1);
     ORCG_ALLOC(uint64_t, seg, 2 * G);
@@ -719,14 +723,6 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
     *d_seg = seg;
     *nseg = G;
     return ORCG_OK;
-  }
-  if (mask) {
-    ORCG_ALLOC(int64_t, counts, G);
-    ORCG_ALLOC(int64_t, pre, G + 1);
-    if ((rc = launch_rg_prefix(ctx, mask, cur_n, cur_rows, G, counts, pre))) return fail_ctx(rc);
-    prefix = pre;
-    seg_prefix = pre;
-    seg_mask = mask;
   }
   ORCG_ALLOC(uint64_t, seg, 2 * G);
   if ((rc = launch_rg_segtab(ctx, (const int64_t*)(D->d_stage + sb.rg_off), prefix, G, boolean, seg)))
@@ -934,6 +930,24 @@ int orcg_reader::queue_dict(uint32_t id, uint64_t n) {
   return ORCG_OK;
 }
 
+int orcg_reader::queue_varint(uint32_t id) {
+  Col& c = H->cols[id];
+  const StreamBuf& sb = c.s[kSlotData];
+  if (!sb.present || sb.len == 0) return ORCG_OK;
+  VarintJob j{};
+  j.src = D->d_stage + sb.host_off;
+  j.len = sb.len;
+  ORCG_ALLOC_TO(int64_t, j.counts, sb.len / kVarintTile + 2);
+  ORCG_ALLOC_TO(int64_t, j.base, sb.len / kVarintTile + 3);
+  const uint64_t* h_total = nullptr;
+  j.total = rb_alloc(1, &h_total);
+  if (!j.total) return ORCG_OK;  // no read-back slot: decode() counts it itself
+  varint_jobs.push_back(j);
+  varint_pre[id] = {j.base, h_total};
+  launches.push_back(MultiLaunch{4, 0, &varint_jobs.back(), 1, 0, 0});
+  return ORCG_OK;
+}
+
 // The streams decode() will read with host-known counts, in its order
 // (same slots, signedness and counts as decode()'s int_stream calls).
 int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
@@ -947,8 +961,12 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
   const uint32_t k = c.kind;
   int rc = ORCG_OK;
   if (k == ORCG_TYPE_DECIMAL) {
-    if (decimal_as_long && footer.types[id].precision - 1u < 18u) rc = queue_stream(id, kSlotData, true, n, true);
-    else rc = queue_stream(id, kSlotSecondary, true, n, false);
+    if (decimal_as_long && footer.types[id].precision - 1u < 18u) {
+      rc = queue_stream(id, kSlotData, true, n, true);
+    } else {
+      rc = queue_stream(id, kSlotSecondary, true, n, false);
+      if (!rc && c.s[kSlotSecondary].present) rc = queue_varint(id);
+    }
   } else if (k == ORCG_TYPE_TIMESTAMP || k == ORCG_TYPE_TIMESTAMP_INSTANT) {
     rc = queue_stream(id, kSlotData, true, n, false);
     if (!rc) rc = queue_stream(id, kSlotSecondary, false, n, false);
@@ -1126,13 +1144,24 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       if ((rc = int_stream(c, kSlotSecondary, true, nonnull, &scales))) return rc;
       const StreamBuf& sb = c.s[kSlotData];
       const uint8_t* d_src = D->d_stage + sb.host_off;
-      uint64_t ntiles = 0;
-      ORCG_ALLOC(int64_t, counts, sb.len / kVarintTile + 2);
-      ORCG_ALLOC(int64_t, base, sb.len / kVarintTile + 3);
-      if ((rc = launch_varint_tile_counts(ctx, d_src, sb.len, counts, &ntiles))) return fail_ctx(rc);
-      if ((rc = launch_exclusive_scan(ctx, counts, ntiles, base))) return fail_ctx(rc);
-      const uint64_t* total = defer(base + ntiles, 1);
-      if (!total) return fail(ORCG_DEVICE_ERROR, "D2H of the varint count failed");
+      int64_t* base = nullptr;
+      const uint64_t* total = nullptr;
+      const auto vp = varint_pre.find(id);
+      if (vp != varint_pre.end()) {
+        // tile counts + scan ran with the batch (queue_varint)
+        base = vp->second.first;
+        total = vp->second.second;
+      } else {
+        uint64_t ntiles = 0;
+        ORCG_ALLOC(int64_t, counts, sb.len / kVarintTile + 2);
+        ORCG_ALLOC_TO(int64_t, base, sb.len / kVarintTile + 3);
+        const uint64_t* h_total = nullptr;
+        uint64_t* d_total = rb_alloc(1, &h_total);
+        if ((rc = launch_varint_tile_counts(ctx, d_src, sb.len, counts, &ntiles))) return fail_ctx(rc);
+        if ((rc = launch_exclusive_scan(ctx, counts, ntiles, base, nullptr, d_total))) return fail_ctx(rc);
+        total = d_total ? h_total : defer(base + ntiles, 1);
+        if (!total) return fail(ORCG_DEVICE_ERROR, "D2H of the varint count failed");
+      }
       F->checks.emplace_back(cur_col, [this, total, nonnull, cid]() -> int {
         return *total < nonnull ? fail(ORCG_PARSE_ERROR, "Read past end of stream in Decimal64ColumnReader column " +
                                                              cid + " kind DATA")
@@ -1327,19 +1356,23 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       const bool rows_placed = row_nn && placed;
       const uint64_t ns = rows_placed ? n : nonnull;
       ORCG_ALLOC(int64_t, dstart, ns + 1);
-      if ((rc = launch_exclusive_scan(ctx, rows_placed ? placed : dlen, ns, dstart))) return fail_ctx(rc);
+      // computeSize's checks (ColumnReader.cc:694-710) ride the scan: a
+      // negative length, the total's overflow (then the blob's size below),
+      // in the reference's order; the flags start at 0 (read-back block)
+      const uint64_t* h_fl = nullptr;
+      uint64_t* flags = rb_alloc(2, &h_fl);
+      if (!flags) {
+        ORCG_ALLOC_TO(uint64_t, flags, 2);
+        if ((rc = hip_check(ctx, hipMemsetAsync(flags, 0, 16, ctx->stream), "flags memset"))) return fail_ctx(rc);
+      }
+      const uint64_t* need = nullptr;
+      uint64_t* d_need = rb_alloc(1, &need);
+      if ((rc = launch_exclusive_scan(ctx, rows_placed ? placed : dlen, ns, dstart, flags, d_need))) return fail_ctx(rc);
       StreamBuf& db = c.s[kSlotData];
       c.blob = D->d_stage + db.host_off;
       c.blob_len = db.len;
-      // computeSize's checks (ColumnReader.cc:694-710) in the reference's
-      // order: a negative length, the total's overflow, then the blob's size
-      const uint64_t* h_fl = nullptr;
-      uint64_t* flags = rb_alloc(2, &h_fl);
-      if (!flags) ORCG_ALLOC_TO(uint64_t, flags, 2);
-      if ((rc = launch_strlen_check(ctx, rows_placed ? placed : dlen, dstart, ns, flags))) return fail_ctx(rc);
       if (!h_fl && !(h_fl = defer(flags, 2))) return fail(ORCG_DEVICE_ERROR, "D2H of the string length checks failed");
-      const uint64_t* need = defer(dstart + ns, 1);
-      if (!need) return fail(ORCG_DEVICE_ERROR, "D2H of the string bytes failed");
+      if (!need && !(need = defer(dstart + ns, 1))) return fail(ORCG_DEVICE_ERROR, "D2H of the string bytes failed");
       const uint64_t blob_len = c.blob_len;
       const uint32_t col_id = cur_col;
       F->checks.emplace_back(cur_col, [this, need, blob_len, h_fl, col_id]() -> int {
@@ -2137,6 +2170,8 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   batched.clear();
   dict_batch.clear();
   dict_done.clear();
+  varint_jobs.clear();
+  varint_pre.clear();
   launches.clear();
   const uint64_t nrows = nrows_stripe;
   const int64_t* rg_rows = hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr;

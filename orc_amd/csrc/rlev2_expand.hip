@@ -51,8 +51,15 @@ __device__ unsigned long long g_xphase[8];
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / kWave;
-constexpr uint32_t kRound = 512;                   // runs per round
-constexpr uint32_t kPer = kSliceMax / kThreads;    // stage values per thread in the scan
+// Slices of kSliceMax values (orcg_internal.hh), kRound runs a round: 18 KB
+// of LDS and <= 80 VGPRs, so 6 workgroups share a CU (the kernel is latency
+// bound: each workgroup waits on a few dependent loads). Measured on
+// configs[3] / [4] (profiles/r06/ab_expand_*): 2,048-value slices with
+// 512-run rounds at 4 workgroups a CU took 102 / 25 us a launch, these 86 /
+// 20 us.
+constexpr uint32_t kRound = 256;
+constexpr int kWavesMin = 6;
+constexpr uint32_t kPer = kSliceMax / kThreads;  // values per thread
 static_assert(kRound * 32 <= kSliceMax * 8, "header staging fits the value stage");
 
 struct Desc {
@@ -89,8 +96,6 @@ __device__ __forceinline__ void store_nt(T* p, uint64_t v) {
   __builtin_nontemporal_store((T)(int64_t)v, p);
 }
 
-// stage slot of value o: one padding slot after every kPer values
-__device__ __forceinline__ uint32_t stage_at(uint32_t o) { return o + o / kPer; }
 
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t x, uint32_t d) {
   const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)x, d), hi = (uint32_t)__shfl_up((int)(uint32_t)(x >> 32), d);
@@ -98,12 +103,14 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t x, uint32_t d) {
 }
 
 template <typename T, bool kMulti>
-__global__ __launch_bounds__(kThreads) void rlev2_expand_kernel(const uint8_t* __restrict__ p_src, uint64_t p_src_len,
+__global__ __launch_bounds__(kThreads, kWavesMin) void rlev2_expand_kernel(const uint8_t* __restrict__ p_src, uint64_t p_src_len,
                                                                 int p_is_signed, uint64_t p_value_begin,
                                                                 uint64_t p_nvalues, T* __restrict__ p_dst,
                                                                 const uint64_t* __restrict__ p_dcount,
                                                                 const RleJob* __restrict__ jobs, uint32_t njobs,
                                                                 const RunTab rt) {
+  // stage slot of value o: one padding slot after every kPer values
+  auto stage_at = [](uint32_t o) -> uint32_t { return o + o / kPer; };
   __shared__ int32_t s_v[kRound];      // run's first value - the slice's first
   __shared__ uint32_t s_meta[kRound];  // kind | W << 2 | L << 9
   __shared__ uint32_t s_dp[kRound];    // descriptor offset of the packed data
@@ -134,6 +141,14 @@ __global__ __launch_bounds__(kThreads) void rlev2_expand_kernel(const uint8_t* _
   const uint64_t vi0 = (uint64_t)uni(hdr[2]) | ((uint64_t)uni(hdr[3]) << 32);
   const uint64_t* tab = rt.tab + uni(hdr[4]);
 
+  // the first round's table entries, requested before the job's fields (the
+  // two loads overlap)
+  uint64_t pre[2] = {0, 0};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint32_t idx = i + (uint32_t)tid + h * kThreads;
+    if (idx < cnt) pre[h] = tab[idx];
+  }
   const uint8_t* src = p_src;
   uint64_t src_len = p_src_len;
   int is_signed = p_is_signed;
@@ -170,7 +185,7 @@ __global__ __launch_bounds__(kThreads) void rlev2_expand_kernel(const uint8_t* _
     for (int h = 0; h < 2; ++h) {
       const uint32_t r = (uint32_t)tid + h * kThreads, idx = i + r;
       if (idx < cnt) {
-        const uint64_t e = tab[idx];
+        const uint64_t e = first ? pre[h] : tab[idx];
         xoff[h] = (uint32_t)e;
         xv[h] = (uint32_t)(e >> 32);
         ok[h] = xv[h] < s0 + slen;
@@ -250,7 +265,9 @@ __global__ __launch_bounds__(kThreads) void rlev2_expand_kernel(const uint8_t* _
     }
     if (carry) __syncthreads();
     // (2) the values, kPer consecutive ones per thread in registers: one
-    //     binary search for the thread's first, then the run cursor advances
+    //     binary search for the thread's first, then the run cursor advances;
+    //     every value's packed bytes are requested before any is used (one
+    //     memory latency per thread instead of one per value)
     const uint32_t q0 = (o_lo & ~(kPer - 1)) + (uint32_t)tid * kPer;
     uint64_t x[kPer];
     uint32_t cov = 0, beg = 0;  // bit e: value q0 + e is covered / starts a scan segment
@@ -263,55 +280,65 @@ __global__ __launch_bounds__(kThreads) void rlev2_expand_kernel(const uint8_t* _
         else hi = mid;
       }
       int32_t vnext = r + 1 < nr ? s_v[r + 1] : 0x7fffffff;
-      uint32_t m = s_meta[r], dp = s_dp[r];
-      int32_t vr = s_v[r];
-      uint64_t a = s_a[r], b = s_b[r];
+      uint32_t re[kPer], je[kPer];
+      u32x3 w[kPer];
+#pragma unroll
+      for (uint32_t e = 0; e < kPer; ++e) {
+        const uint32_t o = q0 + e;
+        while ((int32_t)o >= vnext) {  // the next run (between two tabled runs: the first kernel's values)
+          ++r;
+          vnext = r + 1 < nr ? s_v[r + 1] : 0x7fffffff;
+        }
+        const uint32_t m = s_meta[r], W = (m >> 2) & 127u, L = (m >> 9) & 0x3ffu;
+        const uint32_t j = (uint32_t)((int32_t)o - s_v[r]);
+        const bool in = o >= f0 && o < o_hi && j < L;
+        cov |= in ? 1u << e : 0u;
+        re[e] = r;
+        je[e] = j;
+        // the W-bit field of value j (DELTA: delta j - 2); SHORT_REPEAT and
+        // uncovered values read a harmless in-stream dword
+        const uint32_t kind = m & 3u;
+        const uint32_t k = kind == 3 ? (j >= 2 ? j - 2 : 0u) : j;
+        const uint32_t bit = (in && kind != 0 && W != 0) ? k * W : 0u;
+        const uint32_t y = s_dp[r] + (bit >> 3), ya = y & ~3u;
+        w[e].x = ld32(d, ya);
+        w[e].y = ld32(d, ya + 4);
+        w[e].z = ld32(d, ya + 8);
+      }
 #pragma unroll
       for (uint32_t e = 0; e < kPer; ++e) {
         const uint32_t o = q0 + e;
         x[e] = 0;
-        if (o < f0 || o >= o_hi) {
-          beg |= 1u << e;
-          continue;
-        }
-        if ((int32_t)o >= vnext) {
-          // the next run (values between two tabled runs were expanded by
-          // the first kernel)
-          do {
-            ++r;
-            vnext = r + 1 < nr ? s_v[r + 1] : 0x7fffffff;
-          } while ((int32_t)o >= vnext);
-          m = s_meta[r];
-          dp = s_dp[r];
-          vr = s_v[r];
-          a = s_a[r];
-          b = s_b[r];
-        }
-        const uint32_t kind = m & 3u, W = (m >> 2) & 127u, L = (m >> 9) & 0x3ffu;
-        const uint32_t j = (uint32_t)((int32_t)o - vr);
         bool bg = true;
-        if (j < L) {
-          cov |= 1u << e;
+        if ((cov >> e) & 1u) {
+          const uint32_t rr = re[e], j = je[e];
+          const uint32_t m = s_meta[rr], kind = m & 3u, W = (m >> 2) & 127u;
+          const uint32_t k = kind == 3 ? (j >= 2 ? j - 2 : 0u) : j;
+          const uint32_t bit = k * W, y = s_dp[rr] + (bit >> 3);
+          const uint64_t a = s_a[rr];
           if (kind == 0) {
             x[e] = a;
           } else if (kind == 1) {
-            const uint64_t f = fld(d, dp, j * W, W);
+            const uint64_t f = field(w[e], y, bit & 7u, W);
             x[e] = is_signed ? unzigzag(f) : f;
           } else if (kind == 2) {
-            x[e] = a + fld(d, dp, j * W, W);
-          } else if (W == 0) {
-            x[e] = a + (uint64_t)j * b;
-          } else if (j == 0) {
-            x[e] = a;
-          } else if (o == 0 && carry) {
-            x[e] = s_carry;
-          } else if (j == 1) {
-            x[e] = b;
-            bg = false;
+            x[e] = a + field(w[e], y, bit & 7u, W);
           } else {
-            const uint64_t dl = fld(d, dp, (j - 2) * W, W);
-            x[e] = (int64_t)b < 0 ? 0 - dl : dl;
-            bg = false;
+            const uint64_t b = s_b[rr];
+            if (W == 0) {
+              x[e] = a + (uint64_t)j * b;
+            } else if (j == 0) {
+              x[e] = a;
+            } else if (o == 0 && carry) {
+              x[e] = s_carry;
+            } else if (j == 1) {
+              x[e] = b;
+              bg = false;
+            } else {
+              const uint64_t dl = field(w[e], y, bit & 7u, W);
+              x[e] = (int64_t)b < 0 ? 0 - dl : dl;
+              bg = false;
+            }
           }
         }
         beg |= bg ? 1u << e : 0u;
@@ -434,7 +461,7 @@ int launch_rlev2_expand(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
   if (grid == 0) return ORCG_OK;
   if (grid > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many slices");
   const dim3 g((unsigned)grid), b(kThreads);
-  if (jobs_d) {
+if (jobs_d) {
     hipLaunchKernelGGL((rlev2_expand_kernel<int64_t, true>), g, b, 0, ctx->stream, nullptr, 0, 0, 0, 0, nullptr,
                        nullptr, jobs_d, njobs, rt);
   } else if (dst_bytes == 8) {

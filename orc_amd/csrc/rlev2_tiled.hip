@@ -2349,8 +2349,7 @@ static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
 // ones (at 6 WG/CU they carry 56 B/lane of scratch, the serial ones none), so long-run
 // streams above 1.25 B/value stay on the serial instance.
 static int default_variant(uint64_t src_len, uint64_t est_values) {
-  static const int uv = getenv("ORCG_ONE_PASS") ? 8 : 6;  // TEMP A/B
-  return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : uv);
+  return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 6);
 }
 
 // One launch (or serial + drain pair) of instance `variant` over nsegs
@@ -2376,9 +2375,10 @@ static void debug_defer(Ctx* ctx, const unsigned long long* dq, uint64_t nsegs, 
 // kernel): slices of <= kSliceMax values, a multiple of 256, spg per segment.
 static void two_pass_shape(uint64_t seg_values, uint32_t* spg, uint32_t* slice) {
   const uint64_t n = std::max<uint64_t>(seg_values, 1);
-  const uint64_t k = std::min<uint64_t>((n + kSliceMax - 1) / kSliceMax, 256);
+  const uint64_t smax = kSliceMax;
+  const uint64_t k = std::min<uint64_t>((n + smax - 1) / smax, 256);
   uint64_t s = (n + k - 1) / k;
-  s = std::min<uint64_t>((s + 255) & ~255ull, kSliceMax);
+  s = std::min<uint64_t>((s + 255) & ~255ull, smax);
   *spg = (uint32_t)k;
   *slice = (uint32_t)s;
 }
@@ -2745,6 +2745,11 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
       rc = launch_rlev1_jobs(base, (const V1SegDesc*)m.d_jobs, m.grid, m.variant);
     } else if (m.kind == 2) {
       rc = launch_dict_jobs(base, (const DictJob*)m.d_jobs, m.njobs, m.grid);
+    } else if (m.kind == 4) {
+      const VarintJob& J = *(const VarintJob*)m.d_jobs;
+      uint64_t ntiles = 0;
+      rc = launch_varint_tile_counts(base, J.src, J.len, J.counts, &ntiles);
+      if (!rc) rc = launch_exclusive_scan(base, J.counts, ntiles, J.base, nullptr, J.total);
     } else {
       // a pinned single-stream variant: host job (d_jobs is a host pointer)
       const RleJob& J = *(const RleJob*)m.d_jobs;
