@@ -9,9 +9,8 @@ CSRC = os.path.join(HERE, "csrc")
 # ORCG_PHASE_PROF=1 builds the phase-profiling variant (kernel cycle counters,
 # scripts/phase_prof.py) as liborcgpu_prof.so next to the product library.
 PROF = os.environ.get("ORCG_PHASE_PROF", "") == "1"
-# ORCG_AB=1 builds the A/B variant (every tuning instance of the RLEv2 kernel,
-# RLEv2 variants 8-24, and the device copy probes; scripts/ab_rlev2.py) as
-# liborcgpu_ab.so; the product library carries only the default's instances.
+# ORCG_AB=1 builds the A/B variant (the device copy probes of
+# probe_kernels.hip, scripts/ab_rlev2.py --refs probe5) as liborcgpu_ab.so.
 AB = os.environ.get("ORCG_AB", "") == "1"
 OUT = os.path.join(HERE, "liborcgpu_prof.so" if PROF else ("liborcgpu_ab.so" if AB else "liborcgpu.so"))
 OBJ = os.path.join(HERE, "build_prof" if PROF else ("build_ab" if AB else "build"))
@@ -28,7 +27,6 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-un
 if PROF:
     FLAGS.append("-DORCG_PHASE_PROF")
 if PROF or AB:
-    FLAGS.append("-DORCG_AB_VARIANTS")
     # experiment knobs of the A/B build (e.g. ORCG_AB_FLAGS="-DORCG_ITEM_MAX=1")
     FLAGS.extend(os.environ.get("ORCG_AB_FLAGS", "").split())
 

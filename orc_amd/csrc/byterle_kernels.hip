@@ -123,8 +123,7 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
                                                             uint64_t begin, uint64_t nout, uint8_t* __restrict__ dst,
                                                             unsigned long long* err,
                                                             unsigned long long* __restrict__ ones_total,
-                                                            const uint64_t* __restrict__ d_nout,
-                                                            const RowScatter rsc) {
+                                                            const uint64_t* __restrict__ d_nout) {
 #ifdef ORCG_PHASE_PROF
   uint64_t prof_last_ = wall_clock64();
 #endif
@@ -154,10 +153,7 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
     v_next = segtab[2 * (g + 1) + 1];
   }
   if (seg_end > src_len) seg_end = src_len;
-  // (a segment with nothing to decode still places: its row group's nulls)
-  const bool idle = vi * scale >= end || (v_next != ~0ull && v_next * scale <= begin);
-  if (idle && !rsc.out) return;
-  const uint64_t v0_out = vi * scale;
+  if (vi * scale >= end || (v_next != ~0ull && v_next * scale <= begin)) return;  // nothing to decode
 
   // range-checked descriptor over [seg_start & ~15, end of stream): loads
   // past the stream return zeros
@@ -173,7 +169,7 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
   bool stopped = false;
   uint64_t pos = seg_start;
   const uint32_t cs = (uint32_t)tid * 16u;  // my chunk
-  while (!idle && pos < seg_end && vi < vend) {
+  while (pos < seg_end && vi < vend) {
     const uint32_t wrel = (uint32_t)(pos - bias) & ~15u;
     const uint64_t wpos = bias + wrel;  // stream offset of window byte 0
     for (uint32_t off = (uint32_t)tid * 16u; off < kBWinBytes; off += kBThreads * 16u)
@@ -424,37 +420,25 @@ __global__ __launch_bounds__(kBThreads) void byterle_kernel(const uint8_t* __res
   }
   BPROF_MARK(7);
   if (stopped) return;  // at an error (reported)
-  if (!idle) {
-    if (tid == 0 && v_next != ~0ull && vi < vend && vi != v_next) report(err, vi, kErrBadSegment);
-    // the last segment ran out of stream before the requested values
-    if (tid == 0 && v_next == ~0ull && vi < vend) report(err, vi, kErrByteBadRead);
-  }
-  if (rsc.out) {
-    // RowScatter placement (begin = 0): this segment's outputs [v0, v1)
-    const uint64_t v1 = v_next == ~0ull || v_next * scale > end ? end : v_next * scale;
-    __syncthreads();  // the workgroup's output stores, and its last use of s_win
-    scatter_rows<uint8_t>(rsc, dst, v0_out < v1 ? v0_out : v1, v1, g, s_exit);  // (dead now)
-  }
+  if (tid == 0 && v_next != ~0ull && vi < vend && vi != v_next) report(err, vi, kErrBadSegment);
+  // the last segment ran out of stream before the requested values
+  if (tid == 0 && v_next == ~0ull && vi < vend) report(err, vi, kErrByteBadRead);
 }
 
 }  // namespace
 
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
                    bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst, uint64_t* d_ones,
-                   const uint64_t* d_nout, const RowScatter* rsc_p) {
+                   const uint64_t* d_nout) {
   if (nsegs == 0 || nout == 0) return ORCG_OK;
-  const RowScatter rsc = rsc_p ? *rsc_p : RowScatter{};
-  if (rsc.out && begin) return set_error(ctx, ORCG_INVALID_ARGUMENT, "row placement needs begin = 0");
-  if (rsc.out && ((uintptr_t)rsc.mask & 15u))
-    return set_error(ctx, ORCG_INVALID_ARGUMENT, "row placement needs a 16-byte aligned mask");
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   const dim3 grid((unsigned)nsegs), block(kBThreads);
   if (boolean)
     hipLaunchKernelGGL(byterle_kernel<true>, grid, block, 0, ctx->stream, d_src, src_len, d_segtab, nsegs, begin,
-                       nout, d_dst, ctx->d_err, (unsigned long long*)d_ones, d_nout, rsc);
+                       nout, d_dst, ctx->d_err, (unsigned long long*)d_ones, d_nout);
   else
     hipLaunchKernelGGL(byterle_kernel<false>, grid, block, 0, ctx->stream, d_src, src_len, d_segtab, nsegs, begin,
-                       nout, d_dst, ctx->d_err, (unsigned long long*)nullptr, d_nout, rsc);
+                       nout, d_dst, ctx->d_err, (unsigned long long*)nullptr, d_nout);
   return hip_check(ctx, hipGetLastError(), "byterle_kernel launch");
 }
 

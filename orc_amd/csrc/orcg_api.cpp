@@ -167,11 +167,7 @@ constexpr size_t kHuge = size_t(2) << 20;
 
 void* pinned_alloc(size_t bytes) {
   if (bytes == 0) bytes = 1;
-  static const int mode = [] {  // A/B: ORCG_PIN_MODE=1 always hipHostMalloc
-    const char* e = getenv("ORCG_PIN_MODE");
-    return e ? atoi(e) : 0;
-  }();
-  if (mode == 0 && bytes >= (size_t(8) << 20)) {
+  if (bytes >= (size_t(8) << 20)) {
     const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
     void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m != MAP_FAILED) {
@@ -223,9 +219,18 @@ void pinned_free(void* p) {
   }
 }
 
+// ORCG_DEBUG: comma-separated topics (alloc, stale, rowreader, defer, jobs)
+// whose diagnostics go to stderr
+bool debug_on(const char* topic) {
+  static const std::string topics = [] {
+    const char* e = getenv("ORCG_DEBUG");
+    return std::string(",") + (e ? e : "") + ",";
+  }();
+  return topics.find(std::string(",") + topic + ",") != std::string::npos;
+}
+
 void debug_stale(const char* where) {
-  static const bool on = getenv("ORCG_DEBUG_STALE") != nullptr;
-  if (!on) return;
+  if (!debug_on("stale")) return;
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) fprintf(stderr, "orcg: pending HIP error at %s: %s\n", where, hipGetErrorString(e));
 }

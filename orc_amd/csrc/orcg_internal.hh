@@ -140,6 +140,9 @@ struct V1SegDesc {
 };
 
 int set_error(Ctx* ctx, int status, const std::string& msg);
+// ORCG_DEBUG=topic[,topic...]: stderr diagnostics of that topic (alloc,
+// stale, rowreader, defer, jobs)
+bool debug_on(const char* topic);
 // ORCG_DEBUG_STALE=1: report (and clear) a HIP error left pending on this
 // host thread at `where` (launch checks read hipGetLastError).
 void debug_stale(const char* where);
@@ -163,22 +166,6 @@ int launch_rlev2_decode(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is
                         uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
                         void* d_dst, int dst_bytes, int java = 0);
 
-// Dense -> row placement fused into a decode (out non-null; ColumnReader's
-// null skipping, c++/src/ColumnReader.cc:81-104, RleDecoderV2.cc:437-453):
-// the stream's segments are the row groups of a row-index stream, and the
-// workgroup that decodes segment g also writes the values it decoded to the
-// rows of `mask` they belong to (value index = rank among the set rows) and
-// zeroes the null rows of row group g — no separate scatter launches, and
-// its values are re-read while still in L2. prefix[h] = set rows before row
-// group h (the rg_prefix table the segment table was built from).
-struct RowScatter {
-  const uint8_t* mask;    // non-zero = the row has a value
-  const int64_t* rows;    // first row of each row group (ngroups)
-  const int64_t* prefix;  // ngroups + 1
-  uint64_t nrows;         // the last row group ends here
-  uint64_t ngroups;
-  void* out;              // nrows elements of the decode's output type
-};
 
 // Two-pass short-run RLEv2 decode (DESIGN.md §3.1 "Two passes"): the union
 // instance's dense (short-run) passes write their run starts to `tab` instead
@@ -208,16 +195,14 @@ void warm_rlev2_expand(hipStream_t s);
 
 // RLEv2 kernel variants a context accepts (orcg_rlev2_variants): 0 default,
 // 1 wave-walk, and pins of single tiled instances (launch_rlev2_tiled).
-constexpr int kMaxRlev2Variant = 39;
+constexpr int kMaxRlev2Variant = 8;
 bool rlev2_variant_valid(int v);
 // d_count (may be null): the value count on the device, nvalues then
-// bounds the output only. rsc (may be null): RowScatter placement (segment
-// mode, value_begin 0).
+// bounds the output only.
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues,
-                       void* d_dst, int dst_bytes, const uint64_t* d_count = nullptr,
-                       const RowScatter* rsc = nullptr);
+                       void* d_dst, int dst_bytes, const uint64_t* d_count = nullptr);
 
 // Every stream of `jobs` (segment-table mode, int64 output) in one launch per
 // instance the default's density rule picks (or the pinned variant);
@@ -265,11 +250,10 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& launches);
 
 // d_ones (boolean mode, may be null): += the set rows written (a PRESENT
 // stream's non-null rows), one atomic per wave. d_nout (may be null): the
-// output count on the device (nout then bounds the output only). rsc (may
-// be null, begin 0): RowScatter placement of the decoded bytes / rows.
+// output count on the device (nout then bounds the output only).
 int launch_byterle(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, const uint64_t* d_segtab, uint64_t nsegs,
                    bool boolean, uint64_t begin, uint64_t nout, uint8_t* d_dst, uint64_t* d_ones = nullptr,
-                   const uint64_t* d_nout = nullptr, const RowScatter* rsc = nullptr);
+                   const uint64_t* d_nout = nullptr);
 int launch_rlev1(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed, const uint64_t* d_segtab,
                  uint64_t nsegs, uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes);
 // The segments of several RLEv1 streams (int64 output) in one launch per

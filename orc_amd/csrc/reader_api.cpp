@@ -144,8 +144,7 @@ struct DevPool {
         (void)hipGetLastError();  // the failure must not stick to a later launch check
         if (hipMalloc((void**)&p, bytes) != hipSuccess) {
           (void)hipGetLastError();
-          static const bool dbg = getenv("ORCG_DEBUG_ALLOC") != nullptr;
-          if (dbg) fprintf(stderr, "orcg: device allocation of %zu bytes failed\n", bytes);
+          if (debug_on("alloc")) fprintf(stderr, "orcg: device allocation of %zu bytes failed\n", bytes);
           return nullptr;
         }
         chunks.push_back({p, bytes});
@@ -505,8 +504,7 @@ struct orcg_reader {
     return status;
   }
   int fail_oom(int line) {
-    static const bool dbg = getenv("ORCG_DEBUG_ALLOC") != nullptr;
-    if (dbg) fprintf(stderr, "orcg: reader device allocation failed at reader_api.cpp:%d (column %u)\n", line, cur_col);
+    if (debug_on("alloc")) fprintf(stderr, "orcg: reader device allocation failed at reader_api.cpp:%d (column %u)\n", line, cur_col);
     return fail(ORCG_OUT_OF_MEMORY, "device allocation failed");
   }
 
@@ -577,22 +575,14 @@ struct orcg_reader {
   uint64_t cur_n = 0;
   const uint8_t* cur_in_nn = nullptr;
   const uint8_t* cur_row_nn = nullptr;
-  // segments(): the row-group prefix it built the table from (a masked
-  // row-index stream), else null; with the mask it places the stream's
-  // values at their rows inside the decode (RowScatter)
-  const int64_t* seg_prefix = nullptr;
-  const uint8_t* seg_mask = nullptr;
   int segments(Col& c, int slot, bool boolean, const uint64_t** d_seg, uint64_t* nseg);
-  bool fused_place() const;
   // RLE integer stream: v1 for DIRECT / DICTIONARY encodings (convertRleVersion,
   // DictionaryLoader.hh:42) unless force_v2 (Decimal64ColumnReaderV2 is always RLEv2)
   // (*out: the stream's values, decoded by this stripe's multi-stream batch
   // when collect() queued it, else allocated and decoded now)
   // (dcount: the value count on the device, `count` then only sizes the output)
-  // (placed, may be null: when the decode can place the values at the rows
-  // of cur_row_nn itself, *placed = those cur_n rows (null rows 0), else null)
   int int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** out, bool force_v2 = false,
-                 const uint64_t* dcount = nullptr, int64_t** placed = nullptr);
+                 const uint64_t* dcount = nullptr);
   // Multi-stream batch: before decode(), the RLEv2 streams whose value
   // counts and segments are known without device results (columns with no
   // PRESENT stream, under parents with none) are queued and decoded by one
@@ -623,7 +613,7 @@ struct orcg_reader {
   int queue_dict(uint32_t id, uint64_t n);
   int collect(uint32_t id, uint64_t n, const int64_t* rg_rows);
   int byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones = nullptr,
-                  const uint64_t* d_count = nullptr, uint8_t* place_out = nullptr, bool* placed = nullptr);
+                  const uint64_t* d_count = nullptr);
   int scatter(const void* dense, const uint8_t* nn, uint64_t n, void* out, int width);
   template <typename T>
   T* alloc(uint64_t count) {
@@ -699,8 +689,6 @@ int orcg_reader::scatter(const void* dense, const uint8_t* nn, uint64_t n, void*
 // at each row group's first row (PRESENT streams count the incoming rows).
 int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg, uint64_t* nseg) {
   StreamBuf& sb = c.s[slot];
-  seg_prefix = nullptr;
-  seg_mask = nullptr;
   if (!sb.pos) {
     *d_seg = (const uint64_t*)(D->d_stage + sb.seg_off);
     *nseg = sb.plan->segs.size();
@@ -718,8 +706,6 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
     if ((rc = launch_rg_prefix_segtab(ctx, mask, cur_n, cur_rows, G, (const int64_t*)(D->d_stage + sb.rg_off), boolean,
                                       pre, seg)))
       return fail_ctx(rc);
-    seg_prefix = pre;
-    seg_mask = mask;
     *d_seg = seg;
     *nseg = G;
     return ORCG_OK;
@@ -733,8 +719,7 @@ int orcg_reader::segments(Col& c, int slot, bool boolean, const uint64_t** d_seg
 }
 
 bool orcg_reader::device_counts(const Col& c) const {
-  static const bool off = getenv("ORCG_SYNC_COUNTS") != nullptr;  // A/B: the synchronous counts
-  if (off || !rlev2_multi_capable(ctx->rlev2_variant)) return false;
+  if (!rlev2_multi_capable(ctx->rlev2_variant)) return false;
   const uint32_t k = c.kind;
   if (k == ORCG_TYPE_STRUCT) return true;
   if (c.encoding == kDirect || c.encoding == kDictionary) return false;  // RLEv1
@@ -761,22 +746,8 @@ bool orcg_reader::device_work(uint32_t id) const {
   return true;
 }
 
-// After segments(): the decode can place its values at the rows itself.
-// Off unless ORCG_FUSED_PLACE=1: the row-group segment kernels run one
-// workgroup per row group, and placing inside them costs those launches
-// about what the separate full-chip scatter costs (configs[4]: 3.12-3.26 ms
-// fused vs 3.06-3.11 ms separate, profiles/r05/bench_file_c5_place_ab.json).
-bool orcg_reader::fused_place() const {
-  static const bool on = [] {
-    const char* e = getenv("ORCG_FUSED_PLACE");
-    return e && atoi(e) != 0;
-  }();
-  return on && seg_prefix && seg_mask && cur_rows && H->ngroups;
-}
-
 int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, int64_t** pout, bool force_v2,
-                            const uint64_t* dcount, int64_t** placed) {
-  if (placed) *placed = nullptr;
+                            const uint64_t* dcount) {
   const uint64_t key = (uint64_t)(&c - H->cols.data()) * 8 + (uint64_t)slot;
   const auto it = batched.find(key);
   if (it != batched.end() && it->second.second == count) {
@@ -801,26 +772,11 @@ int orcg_reader::int_stream(Col& c, int slot, bool is_signed, uint64_t count, in
   int rc = segments(c, slot, false, &d_seg, &nseg);
   if (rc) return rc;
   const int sg = is_signed ? 1 : 0;
-  // the values placed at the rows of the column's mask by the decode itself
-  RowScatter rsc{};
-  const bool place = placed && !v1 && ctx->rlev2_variant != ORCG_RLEV2_WAVE_WALK && fused_place() &&
-                     seg_mask == cur_row_nn;
-  static const bool dbg = getenv("ORCG_DEBUG_PLACE") != nullptr;
-  if (dbg && placed)
-    fprintf(stderr, "place: column %u slot %d v1 %d row index %d prefix %d -> %s\n", (unsigned)(&c - H->cols.data()),
-            slot, v1 ? 1 : 0, sb.pos ? 1 : 0, seg_prefix ? 1 : 0, place ? "fused" : "scatter");
-  if (place) {
-    int64_t* rows_out = alloc<int64_t>(cur_n);
-    if (!rows_out) return fail_oom(__LINE__);
-    rsc = RowScatter{seg_mask, cur_rows, seg_prefix, cur_n, H->ngroups, rows_out};
-    *placed = rows_out;
-  }
   madd(kMDecodeCall, 1);
   rc = timed(0, [&]() -> int {
     if (v1) return launch_rlev1(ctx, d_src, sb.len, sg, d_seg, nseg, 0, count, out, 8);
-    return dcount || place ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, dcount,
-                                                place ? &rsc : nullptr)
-                           : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
+    return dcount ? launch_rlev2_tiled(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8, dcount)
+                  : launch_rlev2(ctx, d_src, sb.len, sg, d_seg, nseg, false, 0, 0, count, out, 8);
   });
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
@@ -990,9 +946,8 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
 }
 
 int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uint8_t* out, uint64_t* d_ones,
-                             const uint64_t* d_count, uint8_t* place_out, bool* placed) {
+                             const uint64_t* d_count) {
   StreamBuf& sb = c.s[slot];
-  if (placed) *placed = false;
   if (count == 0) return ORCG_OK;
   if (!sb.present) return fail(ORCG_PARSE_ERROR, "stream not found in column");
   if (!sb.pos && !d_count) {  // (with a device count the kernel reports a short stream)
@@ -1006,17 +961,9 @@ int orcg_reader::byte_stream(Col& c, int slot, bool boolean, uint64_t count, uin
   uint64_t nseg;
   int rc = segments(c, slot, boolean, &d_seg, &nseg);
   if (rc) return rc;
-  // placed at the rows of the incoming mask by the decode itself
-  RowScatter rsc{};
-  const bool place = place_out && slot == kSlotPresent && fused_place() && seg_mask == cur_in_nn;
-  if (place) {
-    rsc = RowScatter{seg_mask, cur_rows, seg_prefix, cur_n, H->ngroups, place_out};
-    *placed = true;
-  }
   madd(kMByteCall, 1);
   rc = timed(1, [&]() -> int {
-    return launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count,
-                          place ? &rsc : nullptr);
+    return launch_byterle(ctx, D->d_stage + sb.host_off, sb.len, d_seg, nseg, boolean, 0, count, out, d_ones, d_count);
   });
   return rc ? fail_ctx(rc) : ORCG_OK;
 }
@@ -1061,14 +1008,10 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     // the decode counts the set rows it writes: the non-null rows, with or
     // without the parent's mask scattered in
     uint64_t* ones = D->d_ones + id;
-    uint8_t* placed_nn = nullptr;
-    if (in_nn) ORCG_ALLOC_TO(uint8_t, placed_nn, n);
-    bool placed = false;
-    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits, ones, d_in, placed_nn, &placed)))
-      return rc;
+    if ((rc = byte_stream(c, kSlotPresent, true, in_nn ? in_count : n, bits, ones, d_in))) return rc;
     if (in_nn) {
-      nn = placed_nn;
-      if (!placed && (rc = scatter(bits, in_nn, n, nn, 1))) return fail_ctx(rc);
+      ORCG_ALLOC_TO(uint8_t, nn, n);
+      if ((rc = scatter(bits, in_nn, n, nn, 1))) return fail_ctx(rc);
     } else {
       nn = bits;
     }
@@ -1129,9 +1072,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (decimal_as_long && t.precision - 1u < 18u) {  // precision 1..18 (0 = Hive 0.11 first)
       // Decimal64ColumnReaderV2 (ColumnReader.cc:1529-1576): RLEv2 unscaled values
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Decimal64V2 column. ColumnId=" + cid);
-      int64_t *dense, *placed;
-      if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, true, nullptr, row_nn ? &placed : nullptr))) return rc;
-      if (!(c.data = row_nn && placed ? placed : place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
+      int64_t* dense;
+      if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, true))) return rc;
+      if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
     } else {
       // Decimal64ColumnReader / Decimal128ColumnReader (:1384-1527): varint
       // DATA, per-value scales in SECONDARY (signed RLE)
@@ -1222,9 +1165,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (!(c.data = place_i64(secs)) || !(c.secondary = place_i64(nanos))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (is_int_kind(k)) {
     if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in Integer column");
-    int64_t *dense, *placed;
-    if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, false, d_nonnull, row_nn ? &placed : nullptr))) return rc;
-    if (!(c.data = row_nn && placed ? placed : place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
+    int64_t* dense;
+    if ((rc = int_stream(c, kSlotData, true, nonnull, &dense, false, d_nonnull))) return rc;
+    if (!(c.data = place_i64(dense))) return fail_ctx(ORCG_DEVICE_ERROR);
   } else if (k == ORCG_TYPE_BOOLEAN || k == ORCG_TYPE_BYTE) {
     if (!has_data)
       return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_BOOLEAN ? "DATA stream not found in Boolean column"
@@ -1324,13 +1267,10 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       });
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDictionaryColumn");
       c.blob = db.present ? D->d_stage + db.host_off : nullptr;
-      int64_t *idx, *placed;
-      if ((rc = int_stream(c, kSlotData, false, nonnull, &idx, false, d_nonnull, row_nn ? &placed : nullptr)))
-        return rc;
+      int64_t* idx;
+      if ((rc = int_stream(c, kSlotData, false, nonnull, &idx, false, d_nonnull))) return rc;
       int64_t* ridx = idx;
-      if (row_nn && placed) {
-        ridx = placed;
-      } else if (row_nn) {
+      if (row_nn) {
         ORCG_ALLOC_TO(int64_t, ridx, n);
         if ((rc = scatter(idx, row_nn, n, ridx, 8))) return fail_ctx(rc);
       }
@@ -1348,13 +1288,9 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     } else {
       if (!has_len) return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDirectColumn");
       if (!has_data) return fail(ORCG_PARSE_ERROR, "DATA stream not found in StringDirectColumn");
-      int64_t *dlen, *placed;
-      if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false, nullptr, row_nn ? &placed : nullptr)))
-        return rc;
-      // lengths placed at the rows by the decode (null rows 0): the scan over
-      // the rows gives every row its start (a null row's is its successor's)
-      const bool rows_placed = row_nn && placed;
-      const uint64_t ns = rows_placed ? n : nonnull;
+      int64_t* dlen;
+      if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false))) return rc;
+      const uint64_t ns = nonnull;
       ORCG_ALLOC(int64_t, dstart, ns + 1);
       // computeSize's checks (ColumnReader.cc:694-710) ride the scan: a
       // negative length, the total's overflow (then the blob's size below),
@@ -1367,7 +1303,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       }
       const uint64_t* need = nullptr;
       uint64_t* d_need = rb_alloc(1, &need);
-      if ((rc = launch_exclusive_scan(ctx, rows_placed ? placed : dlen, ns, dstart, flags, d_need))) return fail_ctx(rc);
+      if ((rc = launch_exclusive_scan(ctx, dlen, ns, dstart, flags, d_need))) return fail_ctx(rc);
       StreamBuf& db = c.s[kSlotData];
       c.blob = D->d_stage + db.host_off;
       c.blob_len = db.len;
@@ -1384,10 +1320,7 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
                       "String length overflow in StringDirectColumnReader for column " + std::to_string(col_id));
         return *need > blob_len ? fail(ORCG_PARSE_ERROR, "failed to read in StringDirectColumnReader.next") : ORCG_OK;
       });
-      if (rows_placed) {
-        start = dstart;
-        len = placed;
-      } else if (row_nn) {
+      if (row_nn) {
         if ((rc = scatter(dstart, row_nn, n, start, 8))) return fail_ctx(rc);
         if ((rc = scatter(dlen, row_nn, n, len, 8))) return fail_ctx(rc);
       } else {
@@ -1401,13 +1334,10 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
     if (!has_len)
       return fail(ORCG_PARSE_ERROR, k == ORCG_TYPE_LIST ? "LENGTH stream not found in List column"
                                                         : "LENGTH stream not found in Map column");
-    int64_t *dlen, *placed;
-    if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false, d_nonnull, row_nn ? &placed : nullptr)))
-      return rc;
+    int64_t* dlen;
+    if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false, d_nonnull))) return rc;
     int64_t* rlen = dlen;
-    if (row_nn && placed) {
-      rlen = placed;
-    } else if (row_nn) {
+    if (row_nn) {
       ORCG_ALLOC_TO(int64_t, rlen, n);
       if ((rc = scatter(dlen, row_nn, n, rlen, 8))) return fail_ctx(rc);
     }
@@ -1606,29 +1536,14 @@ static uint64_t v1_segments(const HostStage& hs) {
 // stripe): stripe footer (Reader.cc getStripeFooter :620-640), stream
 // location (StripeStream.cc:82-125), decompression of every selected stream
 // (Compression.cc) in parallel chunks, run plans + segment tables.
-// Whether an RLEv2 stream's first runs (up to 32) average >= 96 bytes: a
-// stream of long DIRECT / PATCHED_BASE runs (header bytes only are read).
-// A/B (ORCG_SMALL_STREAM=bytes; default 0 = never): streams up to this many
-// bytes take a host plan even with a row index, so their segment table rides
-// in the stripe's upload instead of an rg_segtab launch (+ rg_prefix under a
-// mask) per stream. Measured at 64 KB on configs[0] (9 of its 38 launches
-// per 5,000-row stripe): device decode 0.2337 vs 0.2332 s over the file, the
-// segment-table launches overlap the chain; not the bound, so off.
-static uint64_t small_stream_bytes() {
-  const char* e = getenv("ORCG_SMALL_STREAM");
-  return e ? strtoull(e, nullptr, 10) : 0;
-}
+// (Small streams on host plans instead of row-index segment tables were
+// measured in round 4, profiles/r04/*small_stream_ab*: no gain, dropped.)
 
 // RLEv1 streams up to this size decode in 1 KB host-plan segments
 constexpr uint64_t kV1SmallStream = 64u << 10;
 
-static bool fine_plans() {
-  static const bool on = [] {
-    const char* e = getenv("ORCG_FINE_PLANS");  // A/B: 0 keeps the row index for every RLEv2 stream
-    return !(e && atoi(e) == 0);
-  }();
-  return on;
-}
+// Whether an RLEv2 stream's first runs (up to 32) average >= 96 bytes: a
+// stream of long DIRECT / PATCHED_BASE runs (header bytes only are read).
 static bool long_runs(const uint8_t* p, uint64_t len) {
   uint64_t pos = 0, runs = 0;
   while (pos < len && runs < 32) {
@@ -1885,7 +1800,6 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& 
   // host run plans (header walks only) for every RLE stream, in parallel
   std::vector<StreamBuf*> rle;
   std::vector<int> rle_kind;  // 0 byte RLE, 1 RLEv1, 2 RLEv2
-  const uint64_t small = small_stream_bytes();
   for (size_t i = 0; i < nt; ++i) {
     Col& c = hs.cols[i];
     if (!selected[i] || !c.supported) continue;
@@ -1930,16 +1844,14 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& 
       bool fine = false;
       if (sb.pos) {
         const uint64_t per_group = hs.ngroups ? sb.len / hs.ngroups : 0;
-        if (sb.len <= small) {
-          // small stream: a host plan (small_stream_bytes)
-        } else if (kind == 1 && sb.len <= kV1SmallStream) {
+        if (kind == 1 && sb.len <= kV1SmallStream) {
           // a small RLEv1 stream (configs[0]: 5,000-row stripes, <= 5 KB
           // streams, one row group): 1 KB host-plan segments instead of one
           // row-group segment, so the stream's windows decode side by side
           // (rlev1_kernel's narrow instance) -- the host walk is ~1 ns a byte
         } else if (kind == 0) {
           if (per_group <= (2u << 10)) continue;
-        } else if (kind == 2 && fine_plans() && c.s[kSlotPresent].present && per_group > (8u << 10) &&
+        } else if (kind == 2 && c.s[kSlotPresent].present && per_group > (8u << 10) &&
                    long_runs(hs.h + sb.host_off, sb.len)) {
           fine = true;
         } else {
@@ -1960,13 +1872,8 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& 
     // byte / boolean RLE without row-index segments: 4 KB segments, one
     // byterle_kernel window each (C5's child PRESENT streams: 45.7 -> 32.8 us
     // a launch against 1 KB segments, whose workgroups each paid the
-    // window's fixed phase latencies for a quarter of the bytes;
-    // A/B: ORCG_BYTE_SEG_KB)
-    static const uint32_t byte_seg = [] {
-      const char* e = getenv("ORCG_BYTE_SEG_KB");
-      const int v = e ? atoi(e) : 4;
-      return (uint32_t)std::max(1, std::min(v, 64)) << 10;
-    }();
+    // window's fixed phase latencies for a quarter of the bytes)
+    constexpr uint32_t byte_seg = 4u << 10;
     if (rle_kind[q] == 0) sb.plan.reset(make_byte_plan(p, sb.len, byte_seg, byte_seg));
     else if (rle_kind[q] == 1)
       sb.plan.reset(make_v1_plan(p, sb.len, sb.len <= kV1SmallStream ? (1u << 10) : (16u << 10), 8192));
@@ -2087,8 +1994,7 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   // this stripe's first launch error.
   {
     const hipError_t stale = hipGetLastError();
-    static const bool dbg = getenv("ORCG_DEBUG_STALE") != nullptr;
-    if (dbg && stale != hipSuccess) fprintf(stderr, "orcg: stale HIP error before upload: %s\n", hipGetErrorString(stale));
+    if (debug_on("stale") && stale != hipSuccess) fprintf(stderr, "orcg: stale HIP error before upload: %s\n", hipGetErrorString(stale));
   }
   cur_col = err_col = kNoCol;
   auto early = [&](int rc) {  // a failure before anything was enqueued
@@ -2199,10 +2105,7 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   // (uploaded even after a failure above: finish() reads the records back);
   // a small stripe (configs[0]: ~60 KB) is pulled by a kernel from the
   // pinned staging, a large one copied by the DMA engine
-  static const uint64_t pull_max = [] {
-    const char* e = getenv("ORCG_PULL_BYTES");  // A/B: 0 = always the DMA copy
-    return e ? strtoull(e, nullptr, 10) : (uint64_t)(256u << 10);
-  }();
+  constexpr uint64_t pull_max = 256u << 10;
   if (fl.ev_split && hipEventRecord(fl.ev_up0, ctx->stream) != hipSuccess) fl.ev_split = false;
   const int urc = up <= pull_max && hs.pinned_mapped
                       ? launch_pull(ctx, ds.d_stage, hs.h, up)
@@ -2655,8 +2558,7 @@ struct orcg_row_reader {
         if (rc) err = r->last_error;
         addp(1, t2 - t1);
         addp(2, now_s() - t2);
-        static const bool dbg = getenv("ORCG_DEBUG_ROWREADER") != nullptr;
-        if (dbg)
+        if (debug_on("rowreader"))
           fprintf(stderr, "row reader stripe %llu: prepare %.2f ms, upload+decode %.2f ms (GPU upload %.2f, decode %.2f), "
                   "D2H %.2f ms\n", (unsigned long long)t, (t1 - t0) * 1e3, (t2 - t1) * 1e3,
                   (r->timings[3] - g3) * 1e3, (r->timings[4] - g4) * 1e3, (now_s() - t2) * 1e3);
@@ -3065,13 +2967,7 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
   // the first stripe's decode starts now, on the worker, so the process's
   // first-use costs (code objects, device and pinned allocations: ~40 ms on
   // configs[4]) overlap the caller's setup instead of its first next()
-  // (ORCG_ROWREADER_PREFETCH=0: start at the first next(), as the
-  // reference's RowReaderImpl::startNextStripe does)
-  static const bool prefetch = [] {
-    const char* e = getenv("ORCG_ROWREADER_PREFETCH");
-    return !e || atoi(e) != 0;
-  }();
-  if (prefetch && rr->first < rr->last) {
+  if (rr->first < rr->last) {
     std::unique_lock<std::mutex> lk(rr->m);
     rr->post(lk, rr->first);
   }

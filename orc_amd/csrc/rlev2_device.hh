@@ -202,76 +202,5 @@ __device__ __forceinline__ Run parse_run(ByteFn byte, uint64_t avail, uint32_t l
   return r;
 }
 
-// RowScatter placement by the 256-thread workgroup that decoded segment g
-// (values [v0, v1) of `dense`, in L2 still): each of those values goes to its
-// row (the row whose rank among the set rows of rs.mask is the value index),
-// and the null rows of row group g get 0. The rows scanned run from the row
-// group holding rank v0 (the segment's first run may start in an earlier row
-// group) to the end of row group g, 4096 a round, row t0 + 256 k + tid for k
-// < 16, so mask bytes, dense values and output rows are all accessed
-// coalesced; a row's rank = the round's first rank + the set rows of earlier
-// 256-row chunks + those of lower waves in its chunk (s_tmp: 64 dwords of
-// LDS the caller no longer needs) + a ballot popcount inside its wave.
-// (Measured on configs[4]: this costs the decode launch about as much as the
-// separate full-chip scatter it replaces) Callers run it
-// after a barrier that follows their last value store.
-constexpr uint32_t kScatterLds = 64 * 4;
-template <typename T, typename TD>
-__device__ __forceinline__ void scatter_rows(const RowScatter& rs, const TD* dense, uint64_t v0, uint64_t v1,
-                                             uint64_t g, void* s_tmp_v) {
-  constexpr int kNT = 256, kK = 16;
-  uint32_t* s_tmp = (uint32_t*)s_tmp_v;
-  const int tid = (int)threadIdx.x, lane = tid % kWave, wv = tid / kWave;
-  const uint64_t G = rs.ngroups;
-  if (g >= G) return;
-  auto row_at = [&](uint64_t h) -> uint64_t {
-    const int64_t r = h < G ? rs.rows[h] : (int64_t)rs.nrows;
-    return r < 0 ? 0ull : ((uint64_t)r < rs.nrows ? (uint64_t)r : rs.nrows);
-  };
-  uint64_t h = g;
-  if (v0 < v1)
-    while (h > 0 && (uint64_t)rs.prefix[h] > v0) --h;
-  const uint64_t zero_from = row_at(g), b = row_at(g + 1);
-  uint64_t rank = (uint64_t)rs.prefix[h];
-  T* out = (T*)rs.out;
-  const uint64_t below = (1ull << lane) - 1ull;
-  for (uint64_t t0 = row_at(h); t0 < b; t0 += (uint64_t)kNT * kK) {
-    uint32_t flags = 0, below_cnt[kK];
-#pragma unroll
-    for (int k = 0; k < kK; ++k) {
-      const uint64_t r = t0 + (uint64_t)k * kNT + tid;
-      const bool f = r < b && rs.mask[r] != 0;
-      const uint64_t m = __ballot(f);
-      flags |= (f ? 1u : 0u) << k;
-      below_cnt[k] = (uint32_t)__builtin_popcountll(m & below);
-      if (lane == 0) s_tmp[k * 4 + wv] = (uint32_t)__builtin_popcountll(m);
-    }
-    __syncthreads();
-    uint64_t base = rank;
-#pragma unroll
-    for (int k = 0; k < kK; ++k) {
-      const uint64_t r = t0 + (uint64_t)k * kNT + tid;
-      uint32_t lower = 0, all = 0;
-#pragma unroll
-      for (int w = 0; w < kNT / kWave; ++w) {
-        const uint32_t c = s_tmp[k * 4 + w];
-        lower += w < wv ? c : 0u;
-        all += c;
-      }
-      if (r < b) {
-        if ((flags >> k) & 1u) {
-          const uint64_t v = base + lower + below_cnt[k];
-          if (v >= v0 && v < v1) out[r] = (T)dense[v];
-        } else if (r >= zero_from) {
-          out[r] = (T)0;
-        }
-      }
-      base += all;
-    }
-    rank = base;
-    __syncthreads();  // s_tmp is rewritten by the next round
-  }
-}
-
 }  // namespace dev
 }  // namespace orcg

@@ -60,6 +60,8 @@ constexpr int kWaves = kThreads / kWave;
 constexpr uint32_t kRound = 256;
 constexpr int kWavesMin = 6;
 constexpr uint32_t kPer = kSliceMax / kThreads;  // values per thread
+constexpr int kRunsPer = kRound / kThreads;      // runs per thread in a round
+static_assert(kRunsPer >= 1 && kRunsPer * kThreads == kRound, "whole runs per thread");
 static_assert(kRound * 32 <= kSliceMax * 8, "header staging fits the value stage");
 
 struct Desc {
@@ -143,9 +145,9 @@ __global__ __launch_bounds__(kThreads, kWavesMin) void rlev2_expand_kernel(const
 
   // the first round's table entries, requested before the job's fields (the
   // two loads overlap)
-  uint64_t pre[2] = {0, 0};
+  uint64_t pre[kRunsPer] = {};
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < kRunsPer; ++h) {
     const uint32_t idx = i + (uint32_t)tid + h * kThreads;
     if (idx < cnt) pre[h] = tab[idx];
   }
@@ -179,10 +181,10 @@ __global__ __launch_bounds__(kThreads, kWavesMin) void rlev2_expand_kernel(const
     __syncthreads();
     // (1) the round's runs: table entries i.. that start inside the slice
     //     (sorted by value, so they are a prefix); header bytes to LDS
-    uint32_t xoff[2] = {0, 0}, xv[2] = {0, 0};
-    bool ok[2] = {false, false};
+    uint32_t xoff[kRunsPer] = {}, xv[kRunsPer] = {};
+    bool ok[kRunsPer] = {};
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kRunsPer; ++h) {
       const uint32_t r = (uint32_t)tid + h * kThreads, idx = i + r;
       if (idx < cnt) {
         const uint64_t e = first ? pre[h] : tab[idx];
@@ -206,7 +208,9 @@ __global__ __launch_bounds__(kThreads, kWavesMin) void rlev2_expand_kernel(const
         *(u4*)(s_hb + r * 32u + 16u) = w1;
       }
     }
-    const uint32_t mine = (ok[0] ? 1u : 0u) + (ok[1] ? 1u : 0u);
+    uint32_t mine = 0;
+#pragma unroll
+    for (int h = 0; h < kRunsPer; ++h) mine += ok[h] ? 1u : 0u;
     const uint32_t wtot = wave_scan_u32(mine);
     if (lane == kWave - 1 && wtot) atomicAdd(&s_ctl[0], wtot);
     __syncthreads();
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(kThreads, kWavesMin) void rlev2_expand_kernel(const
     // parse (one thread per run); the staged bytes are dead afterwards
     uint32_t kinds = 0;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kRunsPer; ++h) {
       const uint32_t r = (uint32_t)tid + h * kThreads;
       if (!ok[h]) continue;
       const uint32_t sh = (d.bias + xoff[h]) & 3u;

@@ -819,201 +819,6 @@ __device__ __forceinline__ uint32_t checked_run(const uint32_t* win, uint32_t lq
   return e;
 }
 
-// Discover the runs that start in [sb, sb + lim) of the window (sb = the
-// window offset of `pos`, a run start) into s_off/s_val, with the serial
-// walk's stop rules (segment end, value end, first corrupt run). All threads.
-__device__ __forceinline__ DenseResult dense_discover(const uint32_t* win, uint32_t* s_dp, uint32_t* s_off,
-                                                      uint32_t* s_val, uint16_t* s_nxt, uint32_t* s_mark,
-                                                      uint32_t* s_ctl, uint64_t wpos, uint32_t sb, uint32_t lim,
-                                                      uint64_t vi, uint64_t seg_end, uint64_t src_len,
-                                                      uint64_t value_end, uint32_t need, int is_signed,
-                                                      unsigned long long* err, int tid
-#ifdef ORCG_PHASE_PROF
-                                                      , uint64_t& prof_last_
-#endif
-) {
-  const int wave = tid / kWave, lane = tid % kWave;
-  const uint32_t lo = (uint32_t)tid * kBlk, hi = lo + kBlk;
-  // discovery is a chain of barriers: keep its issue priority above the
-  // expanding waves of co-resident workgroups
-  __builtin_amdgcn_s_setprio(2);
-  // (1) backward scan over the block: s_dp[q] = exit | values << 15, or
-  // kDpErr where the extent parse cannot vouch for the run (corrupt header,
-  // run past the stream / segment / loaded bytes, over-long varints); a
-  // kDpErr on the chain only hands the rest of the slab to the exact walk.
-  {
-    // the block's bytes and 32 more, byte-aligned to the block (sb is
-    // wave-uniform, so is the shift)
-    const uint32_t a0 = sb + lo, sh = a0 & 3u, w0 = a0 >> 2;
-    uint32_t raw[kBlk / 4 + 9], b4[kBlk / 4 + 8];
-#pragma unroll
-    for (int i = 0; i < (int)kBlk / 4 + 9; ++i) raw[i] = win[w0 + i];
-#pragma unroll
-    for (int i = 0; i < (int)kBlk / 4 + 8; ++i) b4[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
-    // terminator mask: bit i = byte i < 0x80 (bytes kBlk .. kBlk + 31 too)
-    uint64_t term = 0;
-#pragma unroll
-    for (int i = 0; i < (int)kBlk / 4 + 8 && i < 16; ++i) {
-      const uint32_t m = (~b4[i] >> 7) & 0x01010101u;
-      term |= (uint64_t)((m * 0x10204080u) >> 28) << (4 * i);
-    }
-    auto B = [&](int i) -> uint32_t { return (b4[i >> 2] >> ((i & 3) * 8)) & 0xffu; };
-#pragma unroll
-    for (int e = (int)kBlk - 1; e >= 0; --e) {
-      const uint32_t q = lo + (uint32_t)e;
-      const uint32_t fb = B(e), b1 = B(e + 1), b2 = B(e + 2), b3 = B(e + 3);
-      const uint32_t kind = fb >> 6;
-      const uint32_t W = fbs_width((fb >> 1) & 0x1fu);
-      const uint32_t L2 = ((fb & 1u) << 8 | b1) + 1u;
-      uint32_t bytes, L;
-      bool ok = true;
-      if (kind == 0) {
-        bytes = 2u + ((fb >> 3) & 7u);
-        L = (fb & 7u) + 3u;
-      } else if (kind == 1) {
-        bytes = 2u + (W * L2 + 7u) / 8u;
-        L = L2;
-      } else if (kind == 2) {
-        const uint32_t bw = (b2 >> 5) + 1u, pbs = fbs_width(b2 & 0x1fu), pgw = (b3 >> 5) + 1u, pl = b3 & 0x1fu;
-        ok = pl != 0 && pbs + pgw <= 64;
-        bytes = 4u + bw + (W * L2 + 7u) / 8u + (closest_fixed_bits(pbs + pgw) * pl + 7u) / 8u;
-        L = L2;
-      } else {
-        const uint32_t Wd = ((fb >> 1) & 0x1fu) ? W : 0u;
-        const uint64_t t1 = term >> (e + 2);
-        const uint32_t n1 = t1 ? (uint32_t)__builtin_ctzll(t1) + 1u : 64u;  // first varint's bytes
-        const uint64_t t2 = n1 < 32 ? t1 >> n1 : 0;
-        const uint32_t n2 = t2 ? (uint32_t)__builtin_ctzll(t2) + 1u : 64u;
-        ok = n1 <= 12 && n2 <= 12 && !(Wd != 0 && L2 < 2);
-        bytes = 2u + n1 + n2 + (Wd ? (Wd * (L2 - 2u) + 7u) / 8u : 0u);
-        L = L2;
-      }
-      const uint32_t lq = sb + q;
-      const uint64_t pabs = wpos + lq;
-      ok = ok && pabs + bytes <= src_len && pabs + bytes <= seg_end && lq + bytes <= need;
-      uint32_t ent;
-      if (!ok) {
-        ent = kDpErr;
-      } else {
-        const uint32_t nx = q + bytes;
-        if (nx >= hi) {
-          ent = nx | (L << 15);
-        } else {
-          const uint32_t t = s_dp[nx];
-          ent = (t & kDpErr) ? kDpErr : t + (L << 15);
-        }
-      }
-      s_dp[q] = ent;
-    }
-  }
-  __syncthreads();
-  PROF_MARK(3);
-  // (2) the chain from position 0 by pointer doubling. N(q) = the first run
-  // start past q's block if a run starts at q (kSink: corrupt / past the
-  // slab). Level i marks N^(2^i) of every marked position and squares N, so
-  // after 8 levels the first 256 chain elements (one per block at most) are
-  // marked. Marks only grow and every marked position is a chain element, so
-  // reading a mark another thread sets in the same level is harmless (marks
-  // are bits of 32-bit words, set with LDS atomics).
-  {
-    uint16_t* na = s_nxt;
-    uint16_t* nb = s_nxt + kSlab;
-#pragma unroll
-    for (uint32_t e = 0; e < kBlk; ++e) {
-      const uint32_t q = lo + e, t = s_dp[q], x = t & 0x7fffu;
-      na[q] = ((t & kDpErr) || x >= lim) ? kSink : (uint16_t)x;
-    }
-    if (tid < (int)(kSlab / 32)) s_mark[tid] = tid == 0;  // position 0 is the chain's start
-    __syncthreads();
-#pragma unroll 1
-    for (int lev = 0; lev < 8; ++lev) {
-#pragma unroll
-      for (uint32_t e = 0; e < kBlk; ++e) {
-        const uint32_t q = lo + e, n = na[q];
-        if (n != kSink) {
-          if ((s_mark[q >> 5] >> (q & 31u)) & 1u) atomicOr(&s_mark[n >> 5], 1u << (n & 31u));
-          nb[q] = na[n];
-        } else {
-          nb[q] = kSink;
-        }
-      }
-      __syncthreads();
-      uint16_t* t = na;
-      na = nb;
-      nb = t;
-    }
-  }
-  PROF_MARK(4);
-  // (3) block b's entry = its marked position; values before it = exclusive
-  // scan of the entries' value counts. Every thread walks its block from its
-  // entry with the exact checks, keeping its (at most 4: every run is >= 2
-  // bytes) run starts in registers, then emits them after the count scan.
-  static_assert(kBlk == 8, "a block's marks are one byte of a mark word");
-  const uint32_t mb = (s_mark[lo >> 5] >> (lo & 31u)) & 0xffu;
-  const uint32_t eb = mb ? lo + (uint32_t)__builtin_ctz(mb) : kNone;
-  const uint32_t cb = (eb != kNone && !(s_dp[eb] & kDpErr)) ? s_dp[eb] >> 15 : 0u;
-  uint32_t* s_wsum = s_ctl + 4;
-  const uint32_t cincl = wave_scan_u32(cb);
-  if (lane == kWave - 1) s_wsum[wave] = cincl;
-  if (tid == 0) {
-    s_ctl[8] = kNone;  // first block whose walk stopped inside it
-    s_ctl[9] = 0;      // last block with an entry
-    s_ctl[3] = 0;      // stop (corrupt run)
-  }
-  __syncthreads();
-  uint32_t vb = cincl - cb;
-  for (int w = 0; w < wave; ++w) vb += s_wsum[w];
-  __syncthreads();  // s_wsum is reused by the run-count scan
-  uint32_t cnt = 0, p = eb, v = vb;
-  uint32_t pk_off = 0;  // run k starts at lo + 3-bit field k
-  uint64_t pk_val = 0;  // ... with its first value at vb + 16-bit field k (<= 3 * 512)
-  if (eb != kNone) {
-    while (p < hi && p < lim && wpos + sb + p < seg_end && vi + v < value_end) {
-      Run r;
-      const uint32_t e = checked_run(win, sb + p, wpos, seg_end, src_len, need, is_signed, &r);
-      if (e != kErrNone) {
-        report(err, vi + v, e);
-        s_ctl[3] = 1;
-        break;
-      }
-      pk_off |= (p - lo) << (3 * cnt);
-      pk_val |= (uint64_t)(v - vb) << (16 * cnt);
-      ++cnt;
-      p += r.bytes;
-      v += r.L;
-    }
-    if (p < hi) atomicMin(&s_ctl[8], (uint32_t)tid);
-    atomicMax(&s_ctl[9], (uint32_t)tid);
-  }
-  // block-wide exclusive scan of the counts
-  const uint32_t incl = wave_scan_u32(cnt);
-  if (lane == kWave - 1) s_wsum[wave] = incl;
-  __syncthreads();
-  uint32_t base = incl - cnt;
-  for (int w = 0; w < wave; ++w) base += s_wsum[w];
-  const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-  {
-    // the pass ends where the first early-stopping block stopped, else at
-    // the exit of the last block with an entry
-    const uint32_t fin = s_ctl[8] != kNone ? s_ctl[8] : s_ctl[9];
-    if ((uint32_t)tid == fin) {
-      s_ctl[1] = p;
-      s_ctl[2] = v;
-    }
-  }
-  // the DP table is dead: the run table may overwrite it (s_dp aliases
-  // s_off/s_val), but only once every thread has walked
-  __syncthreads();
-  for (uint32_t k = 0; k < cnt; ++k) {
-    s_off[base + k] = sb + lo + ((pk_off >> (3 * k)) & 7u);
-    s_val[base + k] = vb + (uint32_t)((pk_val >> (16 * k)) & 0xffffu);
-  }
-  __syncthreads();
-  PROF_MARK(5);
-  __builtin_amdgcn_s_setprio(0);
-  return DenseResult{uni(total), uni(s_ctl[3]), uni(s_ctl[1]), uni(s_ctl[2])};
-}
-
 // ---- dense mode v2 -----------------------------------------------------
 // The same contract as dense_discover, restructured for the CDNA issue model
 // (the v1 code spent ~3.7 SALU instructions per decoded value on exec-mask
@@ -1596,19 +1401,6 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Dense-mode LDS (only instantiated when kDense): block entries and the
-// per-wave value stages.
-template <bool kDense>
-struct DenseLds {
-  union {
-    uint64_t stage[kThreads / kWave][kStage];  // expansion: per-wave value stages
-    uint16_t nxt[2][kSlab];                    // discovery: chain successors (double-buffered)
-  };
-  uint32_t mark[kSlab / 32];                   // discovery: chain marks, one bit per position
-};
-template <>
-struct DenseLds<false> {};
-
 // Dense v2 LDS: the run table (u16 window offsets, u32 value offsets) shares
 // its bytes with the chain's single successor table (dead once the runs are
 // emitted); per-wave value stages; chain marks.
@@ -1639,17 +1431,6 @@ struct Dense2TabLds {
   };
 };
 
-template <bool kDense>
-__device__ __forceinline__ uint16_t* s_dense_nxt(DenseLds<kDense>& d) {
-  if constexpr (kDense) return &d.nxt[0][0];
-  else return nullptr;
-}
-template <bool kDense>
-__device__ __forceinline__ uint32_t* s_dense_mark(DenseLds<kDense>& d) {
-  if constexpr (kDense) return d.mark;
-  else return nullptr;
-}
-
 // Deferral (kDefer): a serial-walk instance (kDefer = 1) whose probe pass
 // finds short runs stops at the end of that pass and records {stamp, byte
 // offset, value index} in the segment's own entry of `defer_q` (3 words per
@@ -1666,7 +1447,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint64_t* __restrict__ p_segtab, uint64_t p_nsegs, uint64_t rows_per_group,
     uint64_t p_value_begin, uint64_t p_nvalues, T* __restrict__ p_dst, unsigned long long* p_err,
     unsigned long long* __restrict__ defer_q, uint32_t defer_par, const RleJob* __restrict__ jobs,
-    uint32_t njobs, const uint64_t* __restrict__ p_dcount, const RowScatter rsc, const RunTab rtab) {
+    uint32_t njobs, const uint64_t* __restrict__ p_dcount, const RunTab rtab) {
   // dense instances get 512 B more so the window's run-start chunk is a
   // whole number of 2 KB slabs (no partially occupied discovery pass)
   constexpr uint32_t kWin = kWinKB * 1024u + (kDense ? 512u : 0u);
@@ -1680,7 +1461,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   constexpr uint32_t kWinS = kUnion ? kWin + (uint32_t)(kWaves * kStage * 8 + kSlab / 8) : kWin;
   constexpr uint32_t kChunkS = kWinS - kMaxRun;
   static_assert(!kUnion || (kWin + 32) % 8 == 0, "stage alignment");
-  static_assert(kWinS + 32 >= kScatterLds, "the window holds the RowScatter tables");
   static_assert(!kDense || kChunk % kSlab == 0, "dense window chunk must be whole slabs");
   constexpr int kBufs = kPipe ? 2 : 1;
   static_assert(!(kDense && kPipe), "dense mode is a non-pipelined instance");
@@ -1692,10 +1472,8 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   __shared__ __attribute__((aligned(16))) uint32_t s_win[kBufs][kWinS / 4 + 8];  // + 32 B: the 12-byte extract may read past a run
   __shared__ uint32_t s_ctl[kBufs][16];
   __shared__ uint32_t s_sync[2][2];  // serial passes: {published runs, claimed runs}, by pass parity
-  __shared__ DenseLds<kDense == 1> s_dense;
   OffT* s_off[kBufs];
   uint32_t* s_val[kBufs];
-  uint32_t* s_tab0 = nullptr;   // v1: the slab DP table (aliases the run table)
   uint16_t* s_nxt2 = nullptr;   // v2: successor table, marks, stages
   uint32_t* s_mark2 = nullptr;
   uint64_t* s_stage2 = nullptr;
@@ -1722,7 +1500,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
       s_off[b] = s_tab[b];
       s_val[b] = s_tab[b] + kCap;
     }
-    s_tab0 = s_tab[0];
     if constexpr (!kPipe) {
       __shared__ uint16_t s_itm[kCap];
       s_items = s_itm;
@@ -1782,8 +1559,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     return gg - uni64(J->seg_base);
   };
 
-  // (kDefer = 1: the segment was queued for the drain, which places it)
-  bool seg_queued = false;
   // one segment, from its start or (queued) from a byte offset / value index
   auto run_segment = [&](const uint64_t gg, const bool queued, const uint64_t q_pos, const uint64_t q_vi) {
   const uint64_t g = bind(gg);
@@ -1977,14 +1752,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
                                 , prof_last_
 #endif
             );
-          } else if constexpr (kDense == 1) {
-            d = dense_discover(s_win[0], s_tab0, (uint32_t*)s_off[0], s_val[0], s_dense_nxt(s_dense),
-                               s_dense_mark(s_dense), s_ctl[0], wpos, sb, lim, vi, seg_end, src_len, value_end, need,
-                               is_signed, err, tid
-#ifdef ORCG_PHASE_PROF
-                               , prof_last_
-#endif
-            );
           }
           n = d.n;
           stop = d.stop;
@@ -2010,9 +1777,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
           }
           if constexpr (kDense != 0) {
             if (!tabled) {
-              uint64_t* stage;
-              if constexpr (kDense == 2) stage = s_stage2 + wave * kStage;
-              else stage = s_dense.stage[wave];
+              uint64_t* const stage = s_stage2 + wave * kStage;
               const uint32_t r0 = (uint32_t)(((uint64_t)n * wave) / kWaves),
                              r1 = (uint32_t)(((uint64_t)n * (wave + 1)) / kWaves);
               dense_expand<kOpt>(s_win[0], kWin / 4 + 8, s_off[0], s_val[0], stage, r0, r1, vi, is_signed,
@@ -2181,7 +1946,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
               if (__hip_atomic_load(any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned long long)defer_par)
                 __hip_atomic_store(any, (unsigned long long)defer_par, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-            seg_queued = true;
             return;
           }
         }
@@ -2251,20 +2015,6 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
   if (tid == 0 && v_next == ~0ull && vi < value_end) report(err, vi, kErrBadRead);  // stream ended early
   };
 
-  // RowScatter placement of single-stream segment g once it is decoded:
-  // its values [segtab value index, the next segment's) go to their rows
-  auto place = [&](const uint64_t g) {
-    if constexpr (!kMulti && !kPositions) {
-      if (!rsc.out) return;
-      uint64_t v1 = g + 1 < p_nsegs ? p_segtab[2 * (g + 1) + 1] : value_end;
-      if (v1 > value_end) v1 = value_end;
-      uint64_t v0 = p_segtab[2 * g + 1];
-      if (v0 > v1) v0 = v1;
-      __syncthreads();  // the workgroup's value stores, and its last use of s_win
-      scatter_rows<T>(rsc, p_dst, v0, v1, g, s_win[0]);
-    }
-  };
-
   if constexpr (kDefer == 2) {
     // the drain: one workgroup per launch-wide segment; a segment the serial
     // launch stamped with this pair's sequence number is decoded from its
@@ -2279,12 +2029,10 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
     const uint64_t q = blockIdx.x;
     if (q >= p_nsegs || uni64(defer_q[3 * q]) != (unsigned long long)defer_par) return;
     run_segment(q, true, uni64(defer_q[3 * q + 1]), uni64(defer_q[3 * q + 2]));
-    place(q);
   } else {
     // (one call site per instance: a second one makes the compiler outline
     // run_segment into a call with a ~700-byte stack frame)
     run_segment(blockIdx.x, false, 0, 0);
-    if (!seg_queued) place(blockIdx.x);
   }
 #ifdef ORCG_PHASE_PROF
   if (kUnion && tid == 0 && blockIdx.x < kWgDurMax) {
@@ -2297,19 +2045,11 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void rlev2_tiled_kernel(
 }  // namespace
 
 // Variants (ctx->rlev2_variant, include/orcg.h): 0 = the density-adaptive
-// default; 2-5 pin one of the instances the default launches (the parity
-// tests run each); 1 = the wave-walk kernel (rlev2_kernels.hip). The
-// tuning experiments of the A/B sweeps (8-24) are compiled only into the A/B
-// build (ORCG_AB=1 python -m orc_amd.build -> liborcgpu_ab.so).
-bool rlev2_variant_valid(int v) {
-  if (v >= 0 && v <= 8) return true;
-#ifdef ORCG_AB_VARIANTS
-  // 28-30 (value-parallel short-run groups) were dropped: wrong on short
-  // runs of wide values (tests/test_gpu_dense.py test_wide_short_runs_vs_oracle)
-  if (v >= 9 && v <= kMaxRlev2Variant && (v < 28 || v > 30)) return true;
-#endif
-  return false;
-}
+// default; 2-8 pin one instance (the parity tests run each: 6 = the union
+// instance in two passes, the default's below 1.25 B/value; 8 = the same in
+// one pass); 1 = the wave-walk kernel (rlev2_kernels.hip). (The round 1-5
+// tuning instances of the A/B sweeps were removed in round 6.)
+bool rlev2_variant_valid(int v) { return v >= 0 && v <= 8; }
 
 static int defer_queue(Ctx* ctx, uint64_t nsegs, unsigned long long** out) {
   // {stamp, byte offset, value index} per launch-wide segment, stamps zeroed
@@ -2358,8 +2098,7 @@ static int default_variant(uint64_t src_len, uint64_t est_values) {
 // ORCG_DEBUG_DEFER: after a serial launch, how many of its segments it
 // queued for the dense drain (stderr; synchronises the stream)
 static void debug_defer(Ctx* ctx, const unsigned long long* dq, uint64_t nsegs, uint32_t dpar) {
-  static const bool on = getenv("ORCG_DEBUG_DEFER") != nullptr;
-  if (!on) return;
+  if (!debug_on("defer")) return;
   std::vector<unsigned long long> h(3 * nsegs + 1);
   if (hipStreamSynchronize(ctx->stream) != hipSuccess ||
       hipMemcpy(h.data(), dq, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
@@ -2423,15 +2162,12 @@ static int runtab_buffers(Ctx* ctx, uint64_t entries, uint64_t nsegs, uint32_t s
 static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t src_len, int is_signed,
                         const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode, uint64_t rows_per_group,
                         uint64_t value_begin, uint64_t nvalues, void* d_dst, int dst_bytes, const RleJob* jobs_d,
-                        uint32_t njobs_d, const uint64_t* dcount = nullptr, const RowScatter* rsc_p = nullptr,
-                        const MultiLaunch* ml = nullptr) {
+                        uint32_t njobs_d, const uint64_t* dcount = nullptr, const MultiLaunch* ml = nullptr) {
   if (nsegs == 0 || nvalues == 0) return ORCG_OK;
-  const RowScatter rsc = rsc_p ? *rsc_p : RowScatter{};
   RunTab rtab{nullptr, nullptr, 0, 0};
   if (variant == 6) {
     // the union instance in two passes, when the run table can address the
-    // stream (u32 entries and offsets) and no in-decode placement is asked
-    // for (RowScatter reads the values the first kernel no longer writes)
+    // stream (u32 entries and offsets)
     uint64_t entries = 0, bound = 0;
     uint32_t spg = 0, slice = 0;
     if (jobs_d) {
@@ -2440,7 +2176,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
         spg = ml->spg;
         slice = ml->slice;
       }
-    } else if (!rsc.out && src_len < 0xffff0000ull && nsegs < 0x7fff0000ull) {
+    } else if (src_len < 0xffff0000ull && nsegs < 0x7fff0000ull) {
       entries = src_len / 2 + nsegs + 1;
       bound = positions_mode ? rows_per_group + 512 : seg_value_bound(nvalues, nsegs);
       two_pass_shape(bound, &spg, &slice);
@@ -2452,10 +2188,6 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
       variant = 8;  // one pass
     }
   }
-  if (rsc.out && (jobs_d || positions_mode || value_begin))
-    return set_error(ctx, ORCG_INVALID_ARGUMENT, "row placement needs a single-stream segment-table launch");
-  if (rsc.out && ((uintptr_t)rsc.mask & 15u))
-    return set_error(ctx, ORCG_INVALID_ARGUMENT, "row placement needs a 16-byte aligned mask");
   if (nsegs > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many segments");
   if (dst_bytes != 8 && dst_bytes != 4 && dst_bytes != 2)
     return set_error(ctx, ORCG_INVALID_ARGUMENT, "dst_bytes must be 8, 4 or 2");
@@ -2473,7 +2205,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
   hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
                      d_src, src_len, sg, d_segtab, nsegs, rows_per_group, value_begin, nvalues, (T*)d_dst, \
-                     ctx->d_err, dq, dpar, jobs_d, njobs_d, dcount, rsc, rtab)
+                     ctx->d_err, dq, dpar, jobs_d, njobs_d, dcount, rtab)
 // single-stream instances (+ the multi-stream one for the default's
 // instances, ORCG_KX; the tuning variants have none, ORCG_KX1)
 #define ORCG_KX1(O, WKB, PIPE, MWV, DNV, DFV, GRIDV)                                 \
@@ -2546,36 +2278,6 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
     }
     case 7: ORCG_DEFERRING(kWide | kOptD3, 33, 1, kSer | kOptD3); break;  // 33 KB serial + dense drain (round-3 default, A/B)
     case 8: ORCG_KX(kSer | kOptD3 | kOptUnion, 8, false, 6, 2, 0, grid_s); break;  // union in one pass (round-5 default)
-#ifdef ORCG_AB_VARIANTS
-    case 9: ORCG_KT(kOptNTStore | kOptReuse, 33, false, 1, false); break;             // 33 KB, 4 WG/CU
-    case 10: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 20, false, 4, true); break;  // dense v1, 20.5 KB
-    case 11: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 12, false, 5, true); break;  // dense v1, 12.5 KB
-    case 12: ORCG_KT(kOptNTStore | kOptFast, 21, true, 3, false); break;               // producer wave, 2 x 21 KB
-    case 13: ORCG_KT(kOptNTStore | kOptFast, 13, true, 4, false); break;               // producer wave, 2 x 13 KB
-    case 14: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill, 33, false, 1, false); break;  // 9 + register fill
-    case 15: ORCG_KT(kOptNTStore | kOptReuse | kOptFast, 8, false, 6, true); break;    // dense v1, 8.5 KB
-    case 16: ORCG_KT(kSer, 21, false, 6, false); break;                                // 21 KB serial, no queue
-    case 17: ORCG_KT(kOptNTStore | kOptReuse | kOptRegFill | kOptT4, 33, false, 1, false); break;  // 14 + T4
-    case 18: ORCG_KT(kSer, 12, false, 5, true); break;                                 // dense v1, 12.5 KB + T4
-    case 19: ORCG_KT(kSer, 8, false, 6, true); break;                                  // dense v1, 8.5 KB + T4
-    case 20: ORCG_KT(kWide, 33, false, 1, false); break;                               // 33 KB serial, no queue
-    case 21: ORCG_KT(kSer, 8, false, 6, 2); break;                                     // dense v2, 8.5 KB
-    case 22: ORCG_KT(kSer, 12, false, 5, 2); break;                                    // dense v2, 12.5 KB
-    case 23: ORCG_KT(kSer, 20, false, 4, 2); break;                                    // dense v2, 20.5 KB
-    case 24: ORCG_KT(kWide, 32, false, 1, 2); break;                                   // dense v2, 32.5 KB
-    case 25: ORCG_KT(kWide | kOptPair, 33, false, 1, false); break;                    // 20 + 16-byte pair stores
-    case 26: ORCG_DEFERRING(kWide | kOptD3 | kOptPair, 33, 1, kSer | kOptD3 | kOptPair); break;  // 2 + pair stores
-    case 27: ORCG_KT(kSer | kOptPair, 21, false, 6, false); break;                     // 16 + pair stores
-    case 31: ORCG_KT(kWide | kOptD3 | kOptPrefetch, 33, false, 1, false); break;      // 2 + next-window prefetch
-    case 32: ORCG_KT(kWide | kOptPrefetch, 24, false, 4, false); break;               // 24 KB + prefetch, 4 WG/CU
-    case 33: ORCG_KT(kWide | kOptPrefetch, 16, false, 5, false); break;               // 16 KB + prefetch, 5 WG/CU
-    case 34: ORCG_KT(kSer | kOptD3 | kOptUnion | kOptScan, 8, false, 6, 2); break;      // union + scan chain
-    case 35: ORCG_KT(kSer | kOptD3 | kOptScan, 8, false, 6, 2); break;                  // dense v3 (4) + scan chain
-    case 36: ORCG_KT(kWide | kOptD3 | kOptPair, 33, false, 1, 0); break;                 // 2 + 16-byte pair stores
-    case 37: ORCG_KT((kWide & ~kOptNTStore) | kOptD3, 33, false, 1, 0); break;          // 2 with plain (temporal) stores
-    case 38: ORCG_KT(kWide | kOptD3 | kOptGrpT, 33, false, 1, 0); break;                 // 2 + temporal short-run group stores
-    case 39: ORCG_KT(kSer | kOptGrpT, 21, false, 6, false); break;                       // 16 + temporal short-run group stores
-#endif
     default: return set_error(ctx, ORCG_INVALID_ARGUMENT, "unknown RLEv2 kernel variant");
   }
 #undef ORCG_DEFERRING
@@ -2589,11 +2291,11 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
 int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,
                        const uint64_t* d_segtab, uint64_t nsegs, bool positions_mode,
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
-                       int dst_bytes, const uint64_t* d_count, const RowScatter* rsc) {
+                       int dst_bytes, const uint64_t* d_count) {
   int variant = ctx->rlev2_variant;
   if (variant == 0) variant = default_variant(src_len, positions_mode ? nsegs * rows_per_group : nvalues);
   return launch_tiled(ctx, variant, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode, rows_per_group,
-                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count, rsc);
+                      value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count);
 }
 
 // Job tables go through a pinned ring mirrored on the device (entries are
@@ -2653,8 +2355,7 @@ int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<M
     if (J.nsegs == 0 || J.nvalues == 0) continue;
     group[pinned ? pinned : default_variant(J.src_len, J.nvalues)].push_back(J);
   }
-  static const bool dbg = getenv("ORCG_DEBUG_JOBS") != nullptr;
-  if (dbg)
+  if (debug_on("jobs"))
     for (int v = 2; v <= 8; ++v)
       for (const RleJob& J : group[v])
         fprintf(stderr, "rle job: instance %d bytes %llu values %llu segments %llu (%.3f B/value)\n", v,
@@ -2733,7 +2434,7 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
       unsigned long long* const own = c->d_err;
       c->d_err = base->d_err;
       rc = launch_tiled(c, m.variant, nullptr, 0, 0, nullptr, m.grid, false, 0, 0, m.values, nullptr, 8,
-                        (const RleJob*)m.d_jobs, m.njobs, nullptr, nullptr, &m);
+                        (const RleJob*)m.d_jobs, m.njobs, nullptr, &m);
       c->d_err = own;
       if (rc) {
         char b[160];

@@ -12,7 +12,7 @@ for spec in ${ABQ_SPECS:-"repeat:12" "repeat:64" "shortdirect:16"}; do
   case $rc in 124|137|134|139) exit $rc;; esac
 done
 if [ -n "${ABQ_FILE:-}" ]; then
-  timeout -k 10 300 env ORCG_DEBUG_JOBS=1 python scripts/bench_file.py --workload $ABQ_FILE --rows ${ABQ_FILE_ROWS:-2000000} --iters 1 --no-cpu-baseline > $OUT/file_$ABQ_FILE.log 2>&1
+  timeout -k 10 300 env ORCG_DEBUG=jobs python scripts/bench_file.py --workload $ABQ_FILE --rows ${ABQ_FILE_ROWS:-2000000} --iters 1 --no-cpu-baseline > $OUT/file_$ABQ_FILE.log 2>&1
   echo "file rc=$?" >> $OUT/status.log
 fi
 exit 0

@@ -139,7 +139,7 @@ def row_reader_leg(path, nrows, stripes_wall):
                            timeout=600)
         if r.returncode != 0:
             raise SystemExit("row reader bench failed: %s" % r.stderr[-500:])
-        if os.environ.get("ORCG_DEBUG_ROWREADER"):
+        if "rowreader" in os.environ.get("ORCG_DEBUG", ""):
             sys.stderr.write("batch %d%s:\n%s" % (cap, " pinned" if extra else "", r.stderr))
         d = json.loads(r.stdout.strip().splitlines()[-1])
         d["vs_read_stripes_wall"] = round(d["seconds"] / max(stripes_wall, 1e-9), 2)

@@ -1,5 +1,5 @@
 import os, sys
-os.environ["ORCG_DEBUG_ALLOC"] = "1"
+os.environ["ORCG_DEBUG"] = "alloc"
 sys.path.insert(0, os.getcwd()); sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
 import orc_amd
 from file_parity import path

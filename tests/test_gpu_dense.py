@@ -444,3 +444,60 @@ def test_two_pass_skew_vs_oracle(long_kind, signed):
                     raise AssertionError("variant %d plan range %d-%d: first mismatch at %d" % (variant, a, b, a + i))
     finally:
         ctx.set_rlev2_variant(0)
+
+
+@pytest.mark.parametrize("signed", [True, False])
+def test_two_pass_many_runs_per_slice(signed):
+    """Value slices holding more runs than one expansion round takes
+    (rlev2_expand.hip kRound): one-value DIRECT runs and 3-value
+    SHORT_REPEAT runs (up to ~1,000 runs per 1,024-value slice), with
+    variable-width DELTA runs between them; variant 6 (two passes) against
+    the oracle and variant 8 (one pass)."""
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(303 + int(signed))
+    vals, kinds, lens = [], [], []
+    total = 0
+    while total < 200_000:
+        r = rng.random()
+        if r < 0.6:
+            k, L = 1, 1
+            v = [int(rng.integers(-8, 8)) if signed else int(rng.integers(0, 16))]
+        elif r < 0.97:
+            k, L = 0, 3
+            v = [int(rng.integers(-50, 50)) if signed else int(rng.integers(0, 100))] * 3
+        else:
+            k, L = 3, int(rng.integers(20, 200))
+            d = rng.integers(0, 30, size=L)
+            d[0], d[1] = 0, max(int(d[1]), 1)
+            start = int(rng.integers(-1000, 1000)) if signed else int(rng.integers(10 ** 6, 2 * 10 ** 6))
+            v = [int(x) for x in start + np.cumsum(d)]
+        vals += v
+        kinds.append(k)
+        lens.append(L)
+        total += L
+    v = np.array(vals, dtype=np.int64)
+    kinds = np.array(kinds, dtype=np.uint8)
+    lens = np.array(lens, dtype=np.uint32)
+    stride = 10_000
+    data, pos = _encode_with_positions(orc_amd, v, signed, kinds, lens, stride)
+    want = oracle.rlev2_decode(data.tobytes(), v.size, signed)
+    np.testing.assert_array_equal(want, v)
+    ctx = orc_amd.default_context(0)
+    d_src = torch.from_numpy(data).cuda()
+    d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+    try:
+        for variant in (0, 6, 8):
+            ctx.set_rlev2_variant(variant)
+            out = torch.zeros(v.size, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, v.size, signed, out)
+            ctx.synchronize()
+            got = out.cpu().numpy()
+            if not np.array_equal(got, v):
+                i = int(np.flatnonzero(got != v)[0])
+                raise AssertionError("variant %d: first mismatch at %d: got %s want %s" % (
+                    variant, i, got[max(0, i - 4):i + 8].tolist(), v[max(0, i - 4):i + 8].tolist()))
+    finally:
+        ctx.set_rlev2_variant(0)

@@ -234,10 +234,7 @@ def test_concurrent_readers_on_stripe_ranges(ctx, name):
 def test_row_index_segments_match_host_plans(ctx, name, monkeypatch):
     """Streams cut at row groups by the ROW_INDEX positions (no host header
     walk) decode exactly like the host-planned segmentation, and both equal
-    pyarrow's ORC C++ reader (the reference) on every decodable field.
-    ORCG_SMALL_STREAM=0 (the default) keeps the row index for these small
-    files' streams."""
-    monkeypatch.setenv("ORCG_SMALL_STREAM", "0")
+    pyarrow's ORC C++ reader (the reference) on every decodable field."""
     r = orc_amd.Reader(path(name), ctx)
     got = [r.read_stripe(s) for s in range(r.num_stripes)]
     stats = r.last_stream_stats()

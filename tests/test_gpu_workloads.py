@@ -115,24 +115,3 @@ def test_workload_stream_batching(ctx, files, name):
         # every integer / length / dictionary stream of the flat schema
         on.read_stripes_device(0, 1)
         assert on.last_stream_stats()["batched"] >= 12
-
-
-def test_fused_row_placement_matches_pyarrow():
-    """The decode kernels' own dense -> row placement (RowScatter, on with
-    ORCG_FUSED_PLACE=1: the RLEv2 and PRESENT decodes write their values to
-    the rows of the null mask themselves, no scatter launches) reads the
-    nested-null configs[4] file and the null-bearing golden files exactly as
-    the separate scatter does. The switch is read once per process: the
-    checks run in a child process."""
-    import subprocess
-    import sys
-
-    here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, ORCG_FUSED_PLACE="1")
-    cmd = [sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", "--timeout", "300",
-           os.path.join(here, "test_gpu_workloads.py") + "::test_workload_every_stripe_matches_pyarrow[c5]",
-           os.path.join(here, "test_gpu_workloads.py") + "::test_workload_stream_batching[c5]",
-           os.path.join(here, "test_gpu_reader.py"), "-k", "c5 or null or Null or nested or list or map or union"]
-    p = subprocess.run(cmd, env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=600)
-    assert p.returncode == 0, p.stdout[-4000:] + p.stderr[-2000:]
-    assert " passed" in p.stdout, p.stdout[-2000:]
