@@ -129,10 +129,11 @@ __device__ __forceinline__ U128 div128_pow10(U128 v, uint32_t k) {
 // 3: as 2 with throwOnHive11DecimalOverflow(false): such a value becomes NULL
 // (keep[k] = 0, value 0; :1646-1677), every other keep[k] = 1.
 template <int kMode>
-__global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
-    const uint8_t* __restrict__ src, uint64_t len, const int64_t* __restrict__ tile_base,
-    const int64_t* __restrict__ scales, uint64_t nvalues, int32_t col_scale, void* __restrict__ out,
-    unsigned long long* err, uint8_t* __restrict__ keep) {
+__device__ __forceinline__ void varint_decimal_tile(const uint8_t* __restrict__ src, uint64_t len,
+                                                    const int64_t* __restrict__ tile_base,
+                                                    const int64_t* __restrict__ scales, uint64_t nvalues,
+                                                    int32_t col_scale, void* __restrict__ out, unsigned long long* err,
+                                                    uint8_t* __restrict__ keep, uint64_t tile) {
   constexpr bool kHive = kMode >= 2;
   __shared__ uint8_t s_bad[kMode == 3 ? kVTile : 1];  // mode 3: the varint ran past 128 bits
   __shared__ uint32_t s_buf[(kLook + kVTile) / 4 + 1];
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
   // int64; Decimal128: the raw 128-bit varint, unzigzagged in pass 2)
   __shared__ uint64_t s_lo[kVTile];
   __shared__ uint64_t s_hi[kMode == 0 ? 1 : kVTile];
-  const uint64_t t0 = (uint64_t)blockIdx.x * kVTile;
+  const uint64_t t0 = tile * kVTile;
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // stage [t0 - kLook, t0 + kVTile) (zero past the stream; bytes before 0 are
   // marked as terminators so the first varint starts at 0)
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
   }
   if (lane == 63) s_wsum[wave] = incl;
   __syncthreads();
-  const uint64_t kt = (uint64_t)tile_base[blockIdx.x];  // value index of the tile's first varint
+  const uint64_t kt = (uint64_t)tile_base[tile];  // value index of the tile's first varint
   uint32_t rk = incl - cnt;
   for (int w = 0; w < wave; ++w) rk += s_wsum[w];
   const uint32_t tile_cnt = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
@@ -308,6 +309,31 @@ __global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
   }
 }
 
+template <int kMode>
+__global__ __launch_bounds__(kVThreads) void varint_decimal_kernel(
+    const uint8_t* __restrict__ src, uint64_t len, const int64_t* __restrict__ tile_base,
+    const int64_t* __restrict__ scales, uint64_t nvalues, int32_t col_scale, void* __restrict__ out,
+    unsigned long long* err, uint8_t* __restrict__ keep) {
+  varint_decimal_tile<kMode>(src, len, tile_base, scales, nvalues, col_scale, out, err, keep, blockIdx.x);
+}
+
+// Several columns' decodes in one launch (the reader's batch: the stripe's
+// decimal columns without nulls, after their SECONDARY streams): workgroup ->
+// job by the jobs' first launch-wide tiles.
+template <int kMode>
+__global__ __launch_bounds__(kVThreads) void varint_decimal_multi_kernel(const DecJob* __restrict__ jobs,
+                                                                         uint32_t njobs) {
+  uint32_t lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].tile0 <= blockIdx.x) lo = mid;
+    else hi = mid - 1;
+  }
+  const DecJob& J = jobs[lo];
+  varint_decimal_tile<kMode>(J.src, J.len, J.tile_base, J.scales, J.nvalues, J.scale, J.out, J.err, nullptr,
+                             blockIdx.x - J.tile0);
+}
+
 // TimestampColumnReader::next (ColumnReader.cc:318-347) for writer == reader
 // time zone rules (no adjustment): secs += epoch; nanos decoded from the
 // trailing-zero code; one second back for negative times with nanos > 999999.
@@ -356,6 +382,17 @@ int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const in
     hipLaunchKernelGGL(varint_decimal_kernel<0>, grid, block, 0, ctx->stream, d_src, len, d_tile_base, d_scales,
                        nvalues, scale, d_out, ctx->d_err, d_keep);
   return hip_check(ctx, hipGetLastError(), "varint_decimal_kernel launch");
+}
+
+int launch_decimal_jobs(Ctx* ctx, const DecJob* d_jobs, uint32_t njobs, uint64_t tiles, int mode) {
+  if (njobs == 0 || tiles == 0) return ORCG_OK;
+  if (tiles > 0x7fffffffull) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many decimal tiles");
+  const dim3 grid((unsigned)tiles), block(kVThreads);
+  if (mode == 1)
+    hipLaunchKernelGGL(varint_decimal_multi_kernel<1>, grid, block, 0, ctx->stream, d_jobs, njobs);
+  else
+    hipLaunchKernelGGL(varint_decimal_multi_kernel<0>, grid, block, 0, ctx->stream, d_jobs, njobs);
+  return hip_check(ctx, hipGetLastError(), "varint_decimal_multi_kernel launch");
 }
 
 int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, int64_t epoch) {

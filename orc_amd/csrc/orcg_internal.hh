@@ -223,7 +223,8 @@ inline int stage_rle_jobs(Ctx* ctx, const RleJob* jobs, uint32_t n, const RleJob
 // jobs; run_multi enqueues the kernels (RLEv2 instances on side lanes).
 struct MultiLaunch {
   int kind;           // 0 RLEv2 instance `variant`, 1 RLEv1, 2 dictionaries, 3 pinned single-stream RLEv2
-                      // (host job), 4 varint tile counts + scan (host VarintJob)
+                      // (host job), 4 varint tile counts + scan (host VarintJob), 5 decimal columns (DecJob
+                      // table, `variant` = the decimal mode)
   int variant;
   const void* d_jobs;
   uint32_t njobs;
@@ -298,6 +299,22 @@ constexpr uint64_t kVarintTile = 4096;
 int launch_varint_decimal(Ctx* ctx, const uint8_t* d_src, uint64_t len, const int64_t* d_tile_base,
                           const int64_t* d_scales, uint64_t nvalues, int32_t scale, int mode, void* d_out,
                           uint8_t* d_keep = nullptr);
+// One decimal column of a batched launch (mode 0 Decimal64 / 1 Decimal128,
+// no nulls): varint DATA, its tile bases, the decoded SECONDARY scales;
+// tile0 = its first launch-wide tile (set by the planner).
+struct DecJob {
+  const uint8_t* src;
+  uint64_t len;
+  const int64_t* tile_base;
+  const int64_t* scales;
+  uint64_t nvalues;
+  void* out;
+  unsigned long long* err;
+  uint64_t tile0;
+  int32_t scale;
+  int32_t pad;
+};
+int launch_decimal_jobs(Ctx* ctx, const DecJob* d_jobs, uint32_t njobs, uint64_t tiles, int mode);
 // TimestampColumnReader value construction, in place.
 int launch_timestamp(Ctx* ctx, int64_t* d_secs, int64_t* d_nanos, uint64_t n, int64_t epoch);
 

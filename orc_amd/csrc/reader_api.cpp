@@ -607,6 +607,11 @@ struct orcg_reader {
   std::deque<VarintJob> varint_jobs;
   std::unordered_map<uint32_t, std::pair<int64_t*, const uint64_t*>> varint_pre;
   int queue_varint(uint32_t id);
+  // varint decimal columns (no nulls, not Hive 0.11) decoded by one launch
+  // per mode after the batch's join (varint_decimal_multi_kernel)
+  std::vector<DecJob> dec_batch[2];
+  std::unordered_map<uint32_t, void*> dec_done;
+  int queue_decimal(uint32_t id, uint64_t n);
   std::vector<MultiLaunch> launches;
   std::unordered_map<uint64_t, std::pair<int64_t*, uint64_t>> batched;  // (column, slot) -> (values, count)
   int queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2);
@@ -742,6 +747,7 @@ bool orcg_reader::device_work(uint32_t id) const {
   }
   if (is_int_kind(k)) return !done(kSlotData);
   if (k == ORCG_TYPE_DOUBLE) return false;  // the stream bytes are the values
+  if (k == ORCG_TYPE_DECIMAL && dec_done.count(id)) return false;  // the batch's decimal launch
   if (is_string_kind(k) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)) return dict_done.count(id) == 0;
   return true;
 }
@@ -904,6 +910,31 @@ int orcg_reader::queue_varint(uint32_t id) {
   return ORCG_OK;
 }
 
+int orcg_reader::queue_decimal(uint32_t id, uint64_t n) {
+  const file::TypeInfo& t = footer.types[id];
+  if (t.precision == 0 || n == 0) return ORCG_OK;  // Hive 0.11: the per-column path (its checks, nulling)
+  const auto vp = varint_pre.find(id);
+  const auto sc = batched.find((uint64_t)id * 8 + (uint64_t)kSlotSecondary);
+  if (vp == varint_pre.end() || sc == batched.end() || sc->second.second != n) return ORCG_OK;
+  const bool wide = t.precision > 18;
+  Col& c = H->cols[id];
+  const StreamBuf& sb = c.s[kSlotData];
+  DecJob j{};
+  j.src = D->d_stage + sb.host_off;
+  j.len = sb.len;
+  j.tile_base = vp->second.first;
+  j.scales = sc->second.first;
+  j.nvalues = n;
+  j.err = D->d_errs + id;
+  j.scale = (int32_t)t.scale;
+  int64_t* out = nullptr;
+  ORCG_ALLOC_TO(int64_t, out, wide ? 2 * n : n);
+  j.out = out;
+  dec_batch[wide ? 1 : 0].push_back(j);
+  dec_done[id] = out;
+  return ORCG_OK;
+}
+
 // The streams decode() will read with host-known counts, in its order
 // (same slots, signedness and counts as decode()'s int_stream calls).
 int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
@@ -922,6 +953,7 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
     } else {
       rc = queue_stream(id, kSlotSecondary, true, n, false);
       if (!rc && c.s[kSlotSecondary].present) rc = queue_varint(id);
+      if (!rc && c.s[kSlotData].present) rc = queue_decimal(id, n);
     }
   } else if (k == ORCG_TYPE_TIMESTAMP || k == ORCG_TYPE_TIMESTAMP_INSTANT) {
     rc = queue_stream(id, kSlotData, true, n, false);
@@ -1110,6 +1142,12 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
                                                              cid + " kind DATA")
                                 : ORCG_OK;
       });
+      const auto dd = dec_done.find(id);
+      if (dd != dec_done.end() && !row_nn) {
+        // decoded by the batch's decimal launch (queue_decimal)
+        c.data = dd->second;
+        return ORCG_OK;
+      }
       ORCG_ALLOC(int64_t, dense, wide ? 2 * nonnull : nonnull);
       // throwOnHive11DecimalOverflow(false): overflowing values become NULL
       const bool nullify = hive11 && !hive11_throw;
@@ -2078,6 +2116,9 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   dict_done.clear();
   varint_jobs.clear();
   varint_pre.clear();
+  dec_batch[0].clear();
+  dec_batch[1].clear();
+  dec_done.clear();
   launches.clear();
   const uint64_t nrows = nrows_stripe;
   const int64_t* rg_rows = hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr;
@@ -2097,6 +2138,21 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
     if (!rc && !dict_batch.empty() &&
         (rc = plan_dict_multi(ctx, dict_batch.data(), (uint32_t)dict_batch.size(), launches)))
       rc = fail_ctx(rc);
+    for (int mode = 0; mode < 2 && !rc; ++mode) {
+      std::vector<DecJob>& g = dec_batch[mode];
+      if (g.empty()) continue;
+      uint64_t tiles = 0;
+      for (DecJob& j : g) {
+        j.tile0 = tiles;
+        tiles += (j.len + kVarintTile - 1) / kVarintTile;
+      }
+      const void* d = nullptr;
+      if ((rc = stage_table(ctx, g.data(), g.size() * sizeof(DecJob), &d))) {
+        rc = fail_ctx(rc);
+        break;
+      }
+      launches.push_back(MultiLaunch{5, mode, d, (uint32_t)g.size(), tiles, 0});
+    }
     ctx->arena_h = ctx->arena_d = nullptr;
     ctx->arena_cap = 0;
   }

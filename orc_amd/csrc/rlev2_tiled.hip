@@ -2092,6 +2092,32 @@ static int default_variant(uint64_t src_len, uint64_t est_values) {
   return src_len >= 5 * est_values ? 2 : (4 * src_len >= 5 * est_values ? 3 : 6);
 }
 
+static int cu_count(Ctx* ctx) {
+  if (ctx->num_cus == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+      cus = 256;
+    ctx->num_cus = cus;
+  }
+  return ctx->num_cus;
+}
+
+// The union instance runs in two passes (kOptTable + rlev2_expand_kernel)
+// when its launch has at most this many segments per CU: a launch of a few
+// segments per CU lasts as long as its slowest segments' discovery +
+// expansion, and balancing the expansion by values pays (configs[3]'s
+// multi-stream launch, 1,336 segments: 297 -> 150 + 86 us; configs[4]'s
+// child streams, 264: 93 -> 57 + 20 us); with many more segments than the
+// chip holds at once, the one-pass instance's expansion already overlaps
+// other workgroups' discovery and the second pass only adds its own latency
+// and the run table's traffic (the stream sweep's 10,000-segment launches:
+// SHORT_REPEAT 12-bit 2,016 GB/s in one pass, 1,267 in two; profiles/r06/
+// sweep_*).
+constexpr uint64_t kTwoPassSegsPerCu = 12;
+static int union_variant(Ctx* ctx, uint64_t nsegs) {
+  return nsegs <= kTwoPassSegsPerCu * (uint64_t)cu_count(ctx) ? 6 : 8;
+}
+
 // One launch (or serial + drain pair) of instance `variant` over nsegs
 // segments of one stream, or (jobs_d) over the launch-wide segments of a
 // device job table.
@@ -2195,12 +2221,7 @@ static int launch_tiled(Ctx* ctx, int variant, const uint8_t* d_src, uint64_t sr
   const int sg = is_signed ? 1 : 0;
   unsigned long long* dq = nullptr;
   uint32_t dpar = 0;
-  if (ctx->num_cus == 0) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
-      cus = 256;
-    ctx->num_cus = cus;
-  }
+  (void)cu_count(ctx);
 
 #define ORCG_K(T, P, O, WKB, PIPE, ML)                                                               \
   hipLaunchKernelGGL((rlev2_tiled_kernel<T, P, O, WKB, PIPE, MW, DN, DF, ML>), grid, block, 0, ctx->stream,   \
@@ -2293,7 +2314,10 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
                        uint64_t rows_per_group, uint64_t value_begin, uint64_t nvalues, void* d_dst,
                        int dst_bytes, const uint64_t* d_count) {
   int variant = ctx->rlev2_variant;
-  if (variant == 0) variant = default_variant(src_len, positions_mode ? nsegs * rows_per_group : nvalues);
+  if (variant == 0) {
+    variant = default_variant(src_len, positions_mode ? nsegs * rows_per_group : nvalues);
+    if (variant == 6) variant = union_variant(ctx, nsegs);
+  }
   return launch_tiled(ctx, variant, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode, rows_per_group,
                       value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count);
 }
@@ -2384,8 +2408,9 @@ int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<M
     const RleJob* d = nullptr;
     const int rc = stage_rle_jobs(ctx, g.data(), (uint32_t)g.size(), &d);
     if (rc) return rc;
-    MultiLaunch m{0, v, d, (uint32_t)g.size(), segs, values};
-    if (v == 6 && entries < 0xffff0000ull) {
+    const int lv = (v == 6 && !pinned) ? union_variant(ctx, segs) : v;
+    MultiLaunch m{0, lv, d, (uint32_t)g.size(), segs, values};
+    if (lv == 6 && entries < 0xffff0000ull) {
       m.tab_entries = entries;
       two_pass_shape(bound, &m.spg, &m.slice);
     }
@@ -2420,7 +2445,7 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
   };
   for (const MultiLaunch& m : ls) {
     if (rc) break;
-    if (m.kind == 2 && !joined && (rc = join())) break;
+    if ((m.kind == 2 || m.kind == 5) && !joined && (rc = join())) break;
     debug_stale("run_multi: before a launch");
     if (m.kind == 0) {
       Ctx* c = base;
@@ -2446,6 +2471,8 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
       rc = launch_rlev1_jobs(base, (const V1SegDesc*)m.d_jobs, m.grid, m.variant);
     } else if (m.kind == 2) {
       rc = launch_dict_jobs(base, (const DictJob*)m.d_jobs, m.njobs, m.grid);
+    } else if (m.kind == 5) {
+      rc = launch_decimal_jobs(base, (const DecJob*)m.d_jobs, m.njobs, m.grid, m.variant);
     } else if (m.kind == 4) {
       const VarintJob& J = *(const VarintJob*)m.d_jobs;
       uint64_t ntiles = 0;
