@@ -175,7 +175,12 @@ int orcg_reader_bench_stripe_decode(orcg_reader* r, uint64_t stripe, uint32_t it
  * Per column, orcg_row_reader_column gives the stripe's column view with
  * HOST pointers into that slab (valid until the next orcg_row_reader_next /
  * seek / destroy) plus the element range [begin, begin + count) of the batch
- * (through list / map offsets and union tags). A row reader keeps its own
+ * (through list / map offsets and union tags). In a row reader's views a
+ * dictionary-encoded string column has index + dict_offsets + blob only
+ * (data / length NULL, as with lazy decoding): the slab carries 8 bytes a row
+ * instead of 24, and the caller looks each row up in the dictionary
+ * (StringDictionaryColumnReader::next, ColumnReader.cc:561-594). A row
+ * reader keeps its own
  * RowReaderOptions (include, lazy decoding) and device memory; it borrows
  * the reader (destroy row readers first), whose decodes it takes turns with. */
 typedef struct orcg_row_reader orcg_row_reader;

@@ -143,21 +143,36 @@ class DataBuffer {
 };
 
 // The copies of one batch, spread over the calling thread and a few helper
-// threads that spin between batches (a batch of 1,024 rows is ~10-30 us of
-// copying; waking sleeping threads per batch would cost more than it saves)
-// and sleep after ~50 us without work. Besides byte copies a task can build a
-// string column's data pointers (the per-row work of StringVectorBatch).
+// threads. The work is cut into byte-balanced contiguous parts and thread t
+// first works through part t: a batch's column layout repeats, so each thread
+// writes the same batch buffers every batch and finds them in its own cache
+// (claims from one shared counter, which moved the buffers between cores
+// batch after batch, measured 63-80 Mrows/s on configs[3] at capacity 1,024
+// against 100-107 for fixed parts). A thread done with its part takes what is
+// left of the others', so a helper the OS has parked does not hold the batch.
+// Helpers spin between batches (a batch of 1,024 rows is ~5-15 us of copying;
+// waking sleeping threads per batch would cost more than it saves) and sleep
+// after ~50 us without work; after a small batch each helper prefetches the
+// slab rows that follow its part, the rows the next batch reads. Besides byte
+// copies a task builds a string column's data pointers (and, from a
+// dictionary, its lengths): the per-row work of StringVectorBatch.
 class CopyPool {
  public:
   struct Task {
     void* dst;
     const void* src;
-    uint64_t bytes;              // kind 0: bytes to copy; kind 1: rows
-    int kind = 0;                // 0 memcpy; 1 dst[i] = base + (len[i] > 0 ? src[i] - shift : 0)
+    uint64_t bytes;              // kind 0: bytes to copy; kinds 1, 2: rows
+    int kind = 0;                // 0 memcpy; 1 dst[i] = base + (len[i] > 0 ? src[i] - shift : 0);
+                                 // 2 dictionary entries src[i]: dst[i] = base + offs[e],
+                                 //   out_len[i] = offs[e + 1] - offs[e] (null rows: base, 0)
     const int64_t* len = nullptr;
     char* base = nullptr;
     int64_t shift = 0;
+    int64_t* out_len = nullptr;  // kind 2
+    const int64_t* offs = nullptr;
+    const char* nn = nullptr;
   };
+  static uint64_t weight(const Task& t) { return t.kind == 0 ? t.bytes : t.kind == 1 ? 16 * t.bytes : 24 * t.bytes; }
   static void exec(const Task& t) {
     if (t.kind == 0) {
       if (t.bytes) memcpy(t.dst, t.src, t.bytes);
@@ -165,10 +180,23 @@ class CopyPool {
     }
     char** d = (char**)t.dst;
     const int64_t* st = (const int64_t*)t.src;
-    for (uint64_t i = 0; i < t.bytes; ++i) d[i] = t.base + (t.len[i] > 0 ? st[i] - t.shift : 0);
+    if (t.kind == 1) {
+      for (uint64_t i = 0; i < t.bytes; ++i) d[i] = t.base + (t.len[i] > 0 ? st[i] - t.shift : 0);
+      return;
+    }
+    for (uint64_t i = 0; i < t.bytes; ++i) {
+      if (t.nn && !t.nn[i]) {
+        d[i] = t.base;
+        t.out_len[i] = 0;
+      } else {
+        const int64_t o = t.offs[st[i]];
+        d[i] = t.base + o;
+        t.out_len[i] = t.offs[st[i] + 1] - o;
+      }
+    }
   }
-  explicit CopyPool(unsigned helpers) {
-    for (unsigned i = 0; i < helpers; ++i) ts_.emplace_back([this] { loop(); });
+  explicit CopyPool(unsigned helpers) : parts_(helpers + 1) {
+    for (unsigned i = 0; i < helpers; ++i) ts_.emplace_back([this, i] { loop(i + 1); });
   }
   ~CopyPool() {
     {
@@ -181,13 +209,10 @@ class CopyPool {
   }
   CopyPool(const CopyPool&) = delete;
   CopyPool& operator=(const CopyPool&) = delete;
-  // run every task (cut into <= 64 KB pieces; pointer tasks count 16 bytes a
-  // row) and return when all are done. (Smaller pieces for small batches
-  // measured slower: 8-16 KB pieces cost configs[4] 40 ms more per 10 M rows
-  // at capacity 1024, the claims and completions contending.)
+  // run every task (cut into <= 64 KB pieces) and return when all are done
   void run(const std::vector<Task>& tasks) {
     uint64_t total = 0;
-    for (const Task& t : tasks) total += t.kind ? 16 * t.bytes : t.bytes;
+    for (const Task& t : tasks) total += weight(t);
     if (ts_.empty() || total < (96u << 10)) {
       for (const Task& t : tasks) exec(t);
       return;
@@ -199,58 +224,104 @@ class CopyPool {
         for (uint64_t o = 0; o < t.bytes; o += piece)
           work_.push_back(Task{(char*)t.dst + o, (const char*)t.src + o, std::min(piece, t.bytes - o)});
       } else {
-        const uint64_t rows = std::max<uint64_t>(piece / 16, 1);
+        const uint64_t rows = piece / 16;
         for (uint64_t o = 0; o < t.bytes; o += rows) {
           Task q = t;
           q.dst = (char**)t.dst + o;
           q.src = (const int64_t*)t.src + o;
-          q.len = t.len + o;
           q.bytes = std::min(rows, t.bytes - o);
+          if (t.len) q.len = t.len + o;
+          if (t.out_len) q.out_len = t.out_len + o;
+          if (t.nn) q.nn = t.nn + o;
           work_.push_back(q);
         }
       }
     }
     const uint64_t n = work_.size();
-    if (n >= 0xffff) {  // (the claim word holds 16 bits of task count)
+    if (n >= kMaxTasks) {
       for (const Task& t : work_) exec(t);
       return;
     }
-    const uint64_t g = ++gen_;
+    // parts: thread t starts on [b_t, b_{t+1}), about total / T bytes each
+    const uint64_t T = parts_.size(), g = ++gen_ & kGenMask;
+    uint64_t acc = 0, b = 0, p = 0;
+    for (uint64_t i = 0; i <= n; ++i) {
+      while (p < T && (i == n || acc >= total * (p + 1) / T)) {
+        parts_[p].w.store((g << 40) | ((i > b ? i : b) << 20) | b, std::memory_order_relaxed);
+        b = std::max(b, i);
+        ++p;
+      }
+      if (i < n) acc += weight(work_[i]);
+    }
+    prefetch_.store(total <= kPrefetchMax, std::memory_order_relaxed);
     done_.store(0, std::memory_order_relaxed);
-    // (generation, task count, next index): a helper that claims an index
-    // of a finished generation sees it and takes nothing
-    claim_.store((g << 48) | (n << 32), std::memory_order_release);
-    if (sleepers_.load(std::memory_order_acquire)) {
+    // seq_cst store and load: with release / acquire this store and the
+    // sleepers_ load may pass each other (a store-buffer reordering) while a
+    // helper going to sleep misses the new generation, and no one wakes it
+    go_.store(g, std::memory_order_seq_cst);
+    if (sleepers_.load(std::memory_order_seq_cst)) {
       std::lock_guard<std::mutex> lk(m_);
       cv_.notify_all();
     }
-    help(g);
-    while (done_.load(std::memory_order_acquire) < n) {
+    std::vector<std::pair<const char*, uint64_t>> none;
+    work(g, 0, none);
+    for (uint32_t spin = 1; done_.load(std::memory_order_acquire) < n; ++spin) {
+      if ((spin & 0xffff) == 0 && sleepers_.load(std::memory_order_seq_cst)) {
+        std::lock_guard<std::mutex> lk(m_);
+        cv_.notify_all();
+      }
     }
   }
 
  private:
-  void help(uint64_t g) {
-    // claims by compare-and-swap: a thread still on an older generation
-    // must not consume an index of the current one
-    uint64_t c = claim_.load(std::memory_order_acquire);
-    for (;;) {
-      const uint64_t cg = c >> 48, cn = (c >> 32) & 0xffff, k = c & 0xffffffffu;
-      if (cg != (g & 0xffff) || k >= cn) return;
-      if (!claim_.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
-      exec(work_[k]);
-      done_.fetch_add(1, std::memory_order_acq_rel);
-      c = claim_.load(std::memory_order_acquire);
+  static constexpr uint64_t kGenMask = (1u << 24) - 1, kMaxTasks = 1u << 20, kPrefetchMax = 512u << 10;
+  // part word: generation (24 bits) | end (20) | next (20); a claim is a
+  // compare-and-swap that checks the generation, so a thread still on an
+  // older batch never takes a task of the current one
+  struct alignas(64) Part {
+    std::atomic<uint64_t> w{0};
+  };
+  void work(uint64_t g, unsigned id, std::vector<std::pair<const char*, uint64_t>>& pf) {
+    const bool want_pf = id && prefetch_.load(std::memory_order_relaxed);
+    uint64_t mine = 0;
+    const unsigned T = (unsigned)parts_.size();
+    for (unsigned j = 0; j < T; ++j) {
+      std::atomic<uint64_t>& w = parts_[(id + j) % T].w;
+      uint64_t c = w.load(std::memory_order_acquire);
+      for (;;) {
+        const uint64_t next = c & 0xfffff, end = (c >> 20) & 0xfffff;
+        if ((c >> 40) != g || next >= end) break;
+        if (!w.compare_exchange_weak(c, c + 1, std::memory_order_acq_rel, std::memory_order_acquire)) continue;
+        const Task& t = work_[next];
+        exec(t);
+        ++mine;
+        if (want_pf && j == 0) {
+          if (t.kind == 0) {
+            pf.push_back({(const char*)t.src + t.bytes, t.bytes});
+          } else {
+            pf.push_back({(const char*)((const int64_t*)t.src + t.bytes), 8 * t.bytes});
+            if (t.len) pf.push_back({(const char*)(t.len + t.bytes), 8 * t.bytes});
+          }
+        }
+        ++c;
+      }
     }
+    if (mine) done_.fetch_add(mine, std::memory_order_acq_rel);
+    // (after the batch is released: the caller returns meanwhile; prefetch
+    // never faults, a range past the slab's end included)
+    for (const auto& r : pf)
+      for (uint64_t o = 0; o < r.second; o += 64) __builtin_prefetch(r.first + o, 0, 3);
+    pf.clear();
   }
-  void loop() {
+  void loop(unsigned id) {
     uint64_t seen = 0;
+    std::vector<std::pair<const char*, uint64_t>> pf;
     for (;;) {
-      uint64_t c = 0;
+      uint64_t g = 0;
       bool got = false;
       for (int spin = 0; spin < 20000; ++spin) {
-        c = claim_.load(std::memory_order_acquire);
-        if ((c >> 48) != (seen & 0xffff) && (c & 0xffffffffu) < ((c >> 32) & 0xffff)) {
+        g = go_.load(std::memory_order_acquire);
+        if (g != seen) {
           got = true;
           break;
         }
@@ -258,24 +329,23 @@ class CopyPool {
       }
       if (!got) {
         std::unique_lock<std::mutex> lk(m_);
-        sleepers_.fetch_add(1, std::memory_order_acq_rel);
-        cv_.wait(lk, [&] {
-          const uint64_t x = claim_.load(std::memory_order_acquire);
-          return stop_ || ((x >> 48) != (seen & 0xffff) && (x & 0xffffffffu) < ((x >> 32) & 0xffff));
-        });
+        sleepers_.fetch_add(1, std::memory_order_seq_cst);
+        cv_.wait(lk, [&] { return stop_ || go_.load(std::memory_order_seq_cst) != seen; });
         sleepers_.fetch_sub(1, std::memory_order_acq_rel);
         if (stop_) return;
-        c = claim_.load(std::memory_order_acquire);
+        g = go_.load(std::memory_order_acquire);
       }
-      seen = c >> 48;
-      help(seen);
+      seen = g;
+      work(g, id, pf);
     }
   }
   std::vector<std::thread> ts_;
   std::vector<Task> work_;
+  std::vector<Part> parts_;
   uint64_t gen_ = 0;
-  std::atomic<uint64_t> claim_{0};
+  std::atomic<uint64_t> go_{0};
   std::atomic<uint64_t> done_{0};
+  std::atomic<bool> prefetch_{false};
   std::atomic<int> sleepers_{0};
   std::atomic<bool> stop_flag_{false};
   std::mutex m_;
@@ -822,11 +892,33 @@ inline void RowReader::fill(uint32_t id, ColumnVectorBatch& b) {
       [[fallthrough]];
     case BatchClass::kString: {
       auto& s = static_cast<StringVectorBatch&>(b);
+      s.data.resize(n);
+      char** d = s.data.data();
+      if (v.index && !v.data) {
+        // dictionary: the slab holds each row's entry; starts and lengths
+        // are looked up in the stripe's dictionary (StringDictionaryColumnReader
+        // ::next, ColumnReader.cc:561-594), whose blob is copied once and
+        // shared by the stripe's batches
+        new_stripe();
+        std::shared_ptr<DataBuffer<char>>& blob = blobs_[id];
+        if (!blob) {
+          blob = std::make_shared<DataBuffer<char>>(r_.getMemoryPool(), v.blob_len);
+          if (v.blob_len) memcpy(blob->data(), v.blob, v.blob_len);
+        }
+        s.length.resize(n);
+        if (n) {
+          CopyPool::Task t{d, (const int64_t*)v.index + first, n, 2};
+          t.base = blob->data();
+          t.out_len = s.length.data();
+          t.offs = (const int64_t*)v.dict_offsets;
+          t.nn = nn;
+          copies_.push_back(t);
+        }
+        break;
+      }
       const int64_t* start = (const int64_t*)v.data + first;  // the slab's (start, length) pairs
       const int64_t* len = (const int64_t*)v.length + first;
       copy(s.length, v.length, n, first);
-      s.data.resize(n);
-      char** d = s.data.data();
       if (v.index) {
         // dictionary: the stripe's blob, copied once and shared by its batches
         new_stripe();

@@ -2479,6 +2479,7 @@ struct orcg_row_reader {
   // [3] slab (re)allocation, [4] look-ahead prepare; [5] caller waits for a
   // slab (orcg_row_reader_timings)
   std::atomic<uint64_t> prof[6] = {};  // nanoseconds
+  uint64_t last_d2h = 0;               // bytes of the last slab copy (debug output)
   void addp(int i, double sec) { prof[i].fetch_add((uint64_t)(sec * 1e9), std::memory_order_relaxed); }
   // the worker's own context (stream, error record, scratch, queues): the
   // caller's context may be driven by its thread while the worker decodes
@@ -2524,8 +2525,16 @@ struct orcg_row_reader {
     std::vector<std::pair<int, uint64_t>> cb;
     for (size_t i = 0; i < sl.out.size(); ++i) {
       if (!sl.out[i].decoded) continue;
+      ColOut& o = sl.out[i];
+      if (o.index && o.dict_offsets && o.kind != ORCG_TYPE_DECIMAL) {
+        // a dictionary column travels as entry + dictionary (8 B a row
+        // instead of 24): the host looks up each row's start and length,
+        // as StringDictionaryColumnReader::next does (ColumnReader.cc:561-594)
+        o.data = nullptr;
+        o.length = nullptr;
+      }
       cb.clear();
-      col_buffers(sl.out[i], r->footer.types[i], cb);
+      col_buffers(o, r->footer.types[i], cb);
       for (auto& x : cb) bufs.push_back(Buf{i, x.first, (const uint8_t*)col_get(sl.out[i], x.first), x.second, 0});
     }
     std::vector<size_t> order(bufs.size());
@@ -2562,6 +2571,8 @@ struct orcg_row_reader {
       sl.cap = ncap;
       addp(3, now_s() - ta);
     }
+    last_d2h = 0;
+    for (const Range& rg : rs) last_d2h += rg.bytes;
     for (const Range& rg : rs) {
       const int rc = hip_check(r->ctx, hipMemcpyAsync(sl.h + rg.hoff, rg.d, rg.bytes, hipMemcpyDeviceToHost,
                                                       r->ctx->stream), "D2H row batch");
@@ -2583,16 +2594,22 @@ struct orcg_row_reader {
     // host work ahead, concurrently with this stripe's decode and copies:
     // decompress stripe t + 1 into the other stage (stripe t - 1 is done
     // with it); prepare reads only the file and this row reader's selection
+    // (when stripe t itself is not prepared yet, as for the first stripe, its
+    // decompression goes first: the two would share the host threads and
+    // delay the first batch)
     std::thread ahead;
     const uint64_t u = t + 1;
-    if (u < last && prepared[u & 1] != u) {
-      prepared[u & 1] = u;
-      ahead = std::thread([this, u] {
-        const double tp = now_s();
-        (void)r->prepare(u, stage[u & 1], selected);  // a failure is kept in the stage
-        addp(4, now_s() - tp);
-      });
-    }
+    auto start_ahead = [&] {
+      if (u < last && prepared[u & 1] != u) {
+        prepared[u & 1] = u;
+        ahead = std::thread([this, u] {
+          const double tp = now_s();
+          (void)r->prepare(u, stage[u & 1], selected);  // a failure is kept in the stage
+          addp(4, now_s() - tp);
+        });
+      }
+    };
+    if (prepared[t & 1] == t) start_ahead();
     {
       std::lock_guard<std::mutex> lk(r->mu);
       orcg_reader::Active act(r, own, selected, lazy_dict);
@@ -2601,6 +2618,7 @@ struct orcg_row_reader {
       if (prepared[t & 1] != t) {
         prepared[t & 1] = t;
         rc = r->prepare(t, hs);
+        start_ahead();
       } else {
         rc = hs.rc;
       }
@@ -2616,8 +2634,9 @@ struct orcg_row_reader {
         addp(2, now_s() - t2);
         if (debug_on("rowreader"))
           fprintf(stderr, "row reader stripe %llu: prepare %.2f ms, upload+decode %.2f ms (GPU upload %.2f, decode %.2f), "
-                  "D2H %.2f ms\n", (unsigned long long)t, (t1 - t0) * 1e3, (t2 - t1) * 1e3,
-                  (r->timings[3] - g3) * 1e3, (r->timings[4] - g4) * 1e3, (now_s() - t2) * 1e3);
+                  "D2H %.2f ms (%.1f MB, %.1f GB/s)\n", (unsigned long long)t, (t1 - t0) * 1e3, (t2 - t1) * 1e3,
+                  (r->timings[3] - g3) * 1e3, (r->timings[4] - g4) * 1e3, (now_s() - t2) * 1e3, last_d2h / 1e6,
+                  last_d2h / 1e9 / std::max(now_s() - t2, 1e-9));
       }
       addp(0, t1 - t0);
       prepared[t & 1] = ~0ull;  // the stage is reused by stripe t + 2

@@ -307,13 +307,16 @@ class Reader:
         check(self._L.orcg_reader_stripe_column(self._h, k, tid, ctypes.byref(v)), self._err)
         return v
 
-    def _column(self, v, t, begin=0, count=None, from_host=False, dict_cache=None):
+    def _column(self, v, t, begin=0, count=None, from_host=False, dict_cache=None, lookup=False):
         """Host copy of elements [begin, begin + count) of a column view (the
         whole column by default; device pointers, or with from_host a row
         reader's host slab): offsets rebased to 0 (the reference's batch
         layout), string starts relative to the copied blob (the dictionary,
         or the span of direct strings the range covers). dict_cache (a dict)
-        keeps a dictionary's host copy for the next batches of the stripe."""
+        keeps a dictionary's host copy for the next batches of the stripe.
+        lookup: a dictionary column given as entries only (a row reader's
+        slab) gets its starts and lengths from the dictionary, as
+        StringDictionaryColumnReader::next does (ColumnReader.cc:561-594)."""
         n = v.num_elements if count is None else count
         k = t.kind
 
@@ -344,6 +347,13 @@ class Reader:
                 blob = cached[1] if cached else self._host(v.blob, v.blob_len, np.uint8, from_host).tobytes()
                 if dict_cache is not None and not cached:
                     dict_cache[key] = (dict_offsets, blob)
+                if lookup and data is None:
+                    data = np.zeros(n, np.int64)
+                    length = np.zeros(n, np.int64)
+                    m = slice(None) if nn is None else nn != 0
+                    e = index[m]
+                    data[m] = dict_offsets[e]
+                    length[m] = dict_offsets[e + 1] - dict_offsets[e]
             elif data is not None and n:
                 live = length > 0
                 lo = int(data[live].min()) if live.any() else 0
@@ -517,6 +527,7 @@ class RowReader:
         check(self._L.orcg_row_reader_create(reader._h, ctypes.byref(opts), ctypes.byref(h)), reader._err)
         self._h = h
         self.tight_numeric = tight_numeric
+        self.lazy_dictionary = bool(lazy_dictionary)
         self._dicts = {}  # the current stripe's dictionaries (host copies)
         self._dict_stripe = None
 
@@ -556,7 +567,8 @@ class RowReader:
             check(self._L.orcg_row_reader_column(self._h, t.id, ctypes.byref(v), ctypes.byref(b), ctypes.byref(c)),
                   self.reader._err)
             if v.decoded:
-                col = self.reader._column(v, t, b.value, c.value, from_host=True, dict_cache=self._dicts)
+                col = self.reader._column(v, t, b.value, c.value, from_host=True, dict_cache=self._dicts,
+                                          lookup=not self.lazy_dictionary)
                 if self.tight_numeric and t.kind in _TIGHT:
                     # RowReaderOptions::setUseTightNumericVector: Byte / Short /
                     # Int / FloatVectorBatch (ColumnReader.cc:1703-1790)
