@@ -40,6 +40,9 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <cstdio>
+#include <pthread.h>
+#include <sched.h>
 #include <limits>
 #include <functional>
 #include <list>
@@ -197,6 +200,43 @@ class CopyPool {
   }
   explicit CopyPool(unsigned helpers) : parts_(helpers + 1) {
     for (unsigned i = 0; i < helpers; ++i) ts_.emplace_back([this, i] { loop(i + 1); });
+    // helpers on the caller's NUMA node (the slabs are placed there too):
+    // a helper the scheduler put on the other socket copies across it (with
+    // threads and slabs left where they fell, configs[4] at capacity 1,024
+    // ranged 69-126 Mrows/s from run to run; placed, 104-109)
+    cpu_set_t cs;
+    if (!ts_.empty() && node_cpus(&cs))
+      for (auto& t : ts_) (void)pthread_setaffinity_np(t.native_handle(), sizeof(cs), &cs);
+  }
+  // the CPUs of the calling thread's NUMA node the process may use
+  static bool node_cpus(cpu_set_t* out) {
+    unsigned cpu = 0, node = 0;
+    cpu_set_t allowed;
+    if (getcpu(&cpu, &node) != 0 || sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return false;
+    char path[64];
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%u/cpulist", node);
+    FILE* f = fopen(path, "r");
+    if (!f) return false;
+    char buf[1024];
+    const bool ok = fgets(buf, sizeof buf, f) != nullptr;
+    fclose(f);
+    if (!ok) return false;
+    CPU_ZERO(out);
+    for (char* p = buf; *p && *p != '\n';) {  // "0-63,128-191"
+      char* e = nullptr;
+      const long a = strtol(p, &e, 10);
+      if (e == p) return false;
+      long b = a;
+      if (*e == '-') {
+        p = e + 1;
+        b = strtol(p, &e, 10);
+        if (e == p) return false;
+      }
+      for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+        if (c >= 0 && CPU_ISSET(c, &allowed)) CPU_SET(c, out);
+      p = *e == ',' ? e + 1 : e;
+    }
+    return CPU_COUNT(out) > 0;
   }
   ~CopyPool() {
     {

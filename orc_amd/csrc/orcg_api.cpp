@@ -4,7 +4,11 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <linux/mempolicy.h>
+#include <sched.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <mutex>
@@ -165,13 +169,22 @@ std::unordered_map<void*, size_t> g_pin_maps;  // registered mappings -> length
 constexpr size_t kHuge = size_t(2) << 20;
 }  // namespace
 
-void* pinned_alloc(size_t bytes) {
+int current_numa_node() {
+  unsigned cpu = 0, node = 0;
+  return getcpu(&cpu, &node) == 0 ? (int)node : -1;
+}
+
+void* pinned_alloc(size_t bytes, int node) {
   if (bytes == 0) bytes = 1;
   if (bytes >= (size_t(8) << 20)) {
     const size_t len = (bytes + kHuge - 1) & ~(kHuge - 1);
     void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m != MAP_FAILED) {
       (void)madvise(m, len, MADV_HUGEPAGE);
+      if (node >= 0 && node < 64) {  // before the faults below place the pages
+        const unsigned long mask = 1ul << node;
+        (void)syscall(SYS_mbind, m, len, MPOL_PREFERRED, &mask, 64ul, 0u);
+      }
       // fault the pages in on a few threads (one write per 4 KB page: a huge
       // page faults whole on its first write, a small one each)
       const size_t pages = len >> 12;

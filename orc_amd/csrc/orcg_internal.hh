@@ -148,7 +148,11 @@ bool debug_on(const char* topic);
 void debug_stale(const char* where);
 // page-locked host memory (transparent huge pages + hipHostRegister for large
 // buffers, hipHostMalloc otherwise); pinned_free takes either kind
-void* pinned_alloc(size_t bytes);
+// node >= 0: large buffers prefer that NUMA node's memory (the node of the
+// thread that will read them)
+void* pinned_alloc(size_t bytes, int node = -1);
+// the NUMA node the calling thread runs on (-1 if unknown)
+int current_numa_node();
 void pinned_free(void* p);
 int hip_check(Ctx* ctx, hipError_t e, const char* what);
 int scratch(Ctx* ctx, int slot, size_t bytes, void** out);

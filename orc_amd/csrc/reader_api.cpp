@@ -2480,6 +2480,10 @@ struct orcg_row_reader {
   // slab (orcg_row_reader_timings)
   std::atomic<uint64_t> prof[6] = {};  // nanoseconds
   uint64_t last_d2h = 0;               // bytes of the last slab copy (debug output)
+  // NUMA node of the thread that created the row reader: the caller's
+  // batch copies read the slabs, so their pages live there (the copy
+  // helpers are placed there too, GpuRowReader.hh CopyPool)
+  int node = -1;
   void addp(int i, double sec) { prof[i].fetch_add((uint64_t)(sec * 1e9), std::memory_order_relaxed); }
   // the worker's own context (stream, error record, scratch, queues): the
   // caller's context may be driven by its thread while the worker decodes
@@ -2567,7 +2571,8 @@ struct orcg_row_reader {
       sl.h = nullptr;
       sl.cap = 0;
       const uint64_t ncap = std::max<uint64_t>(total + (total >> 3), 1 << 20);
-      if (!(sl.h = (uint8_t*)pinned_alloc(ncap))) return r->fail(ORCG_OUT_OF_MEMORY, "pinned row batch allocation failed");
+      if (!(sl.h = (uint8_t*)pinned_alloc(ncap, node)))
+        return r->fail(ORCG_OUT_OF_MEMORY, "pinned row batch allocation failed");
       sl.cap = ncap;
       addp(3, now_s() - ta);
     }
@@ -3007,6 +3012,7 @@ int orcg_row_reader_create(orcg_reader* r, const orcg_row_reader_options* o, orc
   int rc = compute_selection(r, o ? o->include : nullptr, o && o->include ? o->include_len : 0, rr->selected);
   if (rc) return rc;
   rr->lazy_dict = o && o->lazy_dictionary != 0;
+  rr->node = current_numa_node();
   if ((rc = orcg_ctx_create(r->own_ctx->device, &rr->own)) != ORCG_OK)
     return r->fail_user(rc, "row reader context creation failed");
   // the caller's kernel choice, snapshotted once: the worker never reads the
