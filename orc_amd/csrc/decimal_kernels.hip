@@ -144,21 +144,44 @@ __device__ __forceinline__ void varint_decimal_tile(const uint8_t* __restrict__ 
   __shared__ uint64_t s_hi[kMode == 0 ? 1 : kVTile];
   const uint64_t t0 = tile * kVTile;
   const int tid = (int)threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // stage [t0 - kLook, t0 + kVTile) (zero past the stream; bytes before 0 are
-  // marked as terminators so the first varint starts at 0)
-  for (uint32_t o = (uint32_t)tid * 4u; o < kLook + kVTile; o += kVThreads * 4u) {
+  // the tile's first value index and value count (the scan of the tile
+  // counts), then every load the tile needs issued up front: its bytes and
+  // the scales of its values (pass 2's scale loads, one dependent load a
+  // loop trip, made the kernel latency-bound: 60 us a configs[3] stripe)
+  const uint64_t kt = (uint64_t)tile_base[tile];  // value index of the tile's first varint
+  const uint64_t kn = (uint64_t)tile_base[tile + 1];
+  const uint32_t lim = kt >= nvalues ? 0u : (uint32_t)min(min(kn - kt, (uint64_t)kVTile), nvalues - kt);
+  constexpr int kStage = (int)((kLook + kVTile + kVThreads * 4u - 1) / (kVThreads * 4u));
+  constexpr int kScales = (int)(kVTile / kVThreads);
+  uint32_t w[kStage];
+  int32_t sc[kScales];
+#pragma unroll
+  for (int j = 0; j < kStage; ++j) {
+    // stage [t0 - kLook, t0 + kVTile) (zero past the stream; bytes before 0
+    // are marked as terminators so the first varint starts at 0)
+    const uint32_t o = (uint32_t)tid * 4u + (uint32_t)j * kVThreads * 4u;
     const int64_t p = (int64_t)t0 - (int64_t)kLook + o;
-    uint32_t w = 0;
+    w[j] = 0;
+    if (o >= kLook + kVTile) continue;
     if (p >= 0 && (uint64_t)p + 4 <= len) {
-      __builtin_memcpy(&w, src + p, 4);
+      __builtin_memcpy(&w[j], src + p, 4);
     } else {
       for (int i = 0; i < 4; ++i) {
         const int64_t q = p + i;
         const uint32_t b = q < 0 ? 0u : ((uint64_t)q < len ? src[q] : 0x80u);
-        w |= b << (8 * i);
+        w[j] |= b << (8 * i);
       }
     }
-    s_buf[o / 4] = w;
+  }
+#pragma unroll
+  for (int j = 0; j < kScales; ++j) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)j * kVThreads;
+    sc[j] = i < lim ? (int32_t)scales[kt + i] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kStage; ++j) {
+    const uint32_t o = (uint32_t)tid * 4u + (uint32_t)j * kVThreads * 4u;
+    if (o < kLook + kVTile) s_buf[o / 4] = w[j];
   }
   __syncthreads();
   const uint32_t r0 = kLook + (uint32_t)tid * kVPer;  // my bytes in s_buf
@@ -181,10 +204,8 @@ __device__ __forceinline__ void varint_decimal_tile(const uint8_t* __restrict__ 
   }
   if (lane == 63) s_wsum[wave] = incl;
   __syncthreads();
-  const uint64_t kt = (uint64_t)tile_base[tile];  // value index of the tile's first varint
   uint32_t rk = incl - cnt;
   for (int w = 0; w < wave; ++w) rk += s_wsum[w];
-  const uint32_t tile_cnt = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
 
   // pass 1: assemble my varints into the stage
   if (cnt && kt + rk < nvalues) {
@@ -248,11 +269,13 @@ __device__ __forceinline__ void varint_decimal_tile(const uint8_t* __restrict__ 
   }
   __syncthreads();
 
-  // pass 2: rescale the staged values with their scales; loads and stores coalesced
-  const uint32_t lim = kt >= nvalues ? 0u : (uint32_t)min((uint64_t)tile_cnt, nvalues - kt);
-  for (uint32_t i = (uint32_t)tid; i < lim; i += kVThreads) {
+  // pass 2: rescale the staged values with their scales; stores coalesced
+#pragma unroll
+  for (int j = 0; j < kScales; ++j) {
+    const uint32_t i = (uint32_t)tid + (uint32_t)j * kVThreads;
+    if (i >= lim) break;
     const uint64_t k = kt + i;
-    const int32_t cur = (int32_t)scales[k];
+    const int32_t cur = sc[j];
     if constexpr (kMode == 0) {
       int64_t v = (int64_t)s_lo[i];
       if (col_scale > cur && (uint64_t)(uint32_t)(col_scale - cur) <= 18) {

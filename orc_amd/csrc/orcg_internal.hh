@@ -228,7 +228,8 @@ inline int stage_rle_jobs(Ctx* ctx, const RleJob* jobs, uint32_t n, const RleJob
 struct MultiLaunch {
   int kind;           // 0 RLEv2 instance `variant`, 1 RLEv1, 2 dictionaries, 3 pinned single-stream RLEv2
                       // (host job), 4 varint tile counts + scan (host VarintJob), 5 decimal columns (DecJob
-                      // table, `variant` = the decimal mode)
+                      // table, `variant` = the decimal mode), 6 a direct string column's length scan (host
+                      // ScanJob)
   int variant;
   const void* d_jobs;
   uint32_t njobs;
@@ -249,6 +250,16 @@ struct VarintJob {
   int64_t* counts;
   int64_t* base;    // ntiles + 1
   uint64_t* total;  // the values in the stream (read-back slot)
+};
+// A direct string column's starts: the exclusive scan of its batched LENGTH
+// stream with computeSize's checks (launch_exclusive_scan's flags / total),
+// run after the join beside the dictionaries and decimals.
+struct ScanJob {
+  const int64_t* in;
+  uint64_t n;
+  int64_t* out;     // n + 1
+  uint64_t* flags;  // 2 (read-back slots)
+  uint64_t* total;  // read-back slot
 };
 int plan_rlev1_multi(Ctx* ctx, const V1SegDesc* segs, uint64_t nsegs, std::vector<MultiLaunch>& out);
 int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& launches);

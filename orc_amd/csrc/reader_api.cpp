@@ -612,6 +612,17 @@ struct orcg_reader {
   std::vector<DecJob> dec_batch[2];
   std::unordered_map<uint32_t, void*> dec_done;
   int queue_decimal(uint32_t id, uint64_t n);
+  // direct string columns (no nulls) whose length scan runs after the
+  // batch's join, beside the dictionaries and decimals
+  struct ScanDone {
+    int64_t* starts;
+    const uint64_t* h_flags;
+    const uint64_t* h_need;
+    uint64_t n;
+  };
+  std::deque<ScanJob> scan_jobs;
+  std::unordered_map<uint32_t, ScanDone> scan_done;
+  int queue_scan(uint32_t id, uint64_t n);
   std::vector<MultiLaunch> launches;
   std::unordered_map<uint64_t, std::pair<int64_t*, uint64_t>> batched;  // (column, slot) -> (values, count)
   int queue_stream(uint32_t id, int slot, bool is_signed, uint64_t count, bool force_v2);
@@ -935,6 +946,22 @@ int orcg_reader::queue_decimal(uint32_t id, uint64_t n) {
   return ORCG_OK;
 }
 
+int orcg_reader::queue_scan(uint32_t id, uint64_t n) {
+  const auto li = batched.find((uint64_t)id * 8 + kSlotLength);
+  if (n == 0 || li == batched.end() || li->second.second != n || !H->cols[id].s[kSlotData].present) return ORCG_OK;
+  ScanJob j{};
+  j.in = li->second.first;
+  j.n = n;
+  ORCG_ALLOC_TO(int64_t, j.out, n + 1);
+  const uint64_t *h_fl = nullptr, *h_need = nullptr;
+  j.flags = rb_alloc(2, &h_fl);
+  j.total = j.flags ? rb_alloc(1, &h_need) : nullptr;
+  if (!j.total) return ORCG_OK;  // no read-back slots: decode() scans it itself
+  scan_jobs.push_back(j);
+  scan_done[id] = ScanDone{j.out, h_fl, h_need, n};
+  return ORCG_OK;
+}
+
 // The streams decode() will read with host-known counts, in its order
 // (same slots, signedness and counts as decode()'s int_stream calls).
 int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
@@ -967,6 +994,7 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
       if (!rc) rc = queue_dict(id, n);
     } else {
       rc = queue_stream(id, kSlotLength, false, n, false);
+      if (!rc) rc = queue_scan(id, n);
     }
   } else if (k == ORCG_TYPE_LIST || k == ORCG_TYPE_MAP) {
     rc = queue_stream(id, kSlotLength, false, n, false);
@@ -1329,19 +1357,30 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       int64_t* dlen;
       if ((rc = int_stream(c, kSlotLength, false, nonnull, &dlen, false))) return rc;
       const uint64_t ns = nonnull;
-      ORCG_ALLOC(int64_t, dstart, ns + 1);
       // computeSize's checks (ColumnReader.cc:694-710) ride the scan: a
       // negative length, the total's overflow (then the blob's size below),
-      // in the reference's order; the flags start at 0 (read-back block)
+      // in the reference's order; the flags start at 0 (read-back block).
+      // The batch's scan (queue_scan) already ran for a column without nulls.
+      const auto sd = scan_done.find(id);
+      const bool pre = sd != scan_done.end() && !row_nn && sd->second.n == ns;
+      int64_t* dstart = nullptr;
       const uint64_t* h_fl = nullptr;
-      uint64_t* flags = rb_alloc(2, &h_fl);
-      if (!flags) {
-        ORCG_ALLOC_TO(uint64_t, flags, 2);
-        if ((rc = hip_check(ctx, hipMemsetAsync(flags, 0, 16, ctx->stream), "flags memset"))) return fail_ctx(rc);
-      }
       const uint64_t* need = nullptr;
-      uint64_t* d_need = rb_alloc(1, &need);
-      if ((rc = launch_exclusive_scan(ctx, dlen, ns, dstart, flags, d_need))) return fail_ctx(rc);
+      uint64_t* flags = nullptr;
+      if (pre) {
+        dstart = sd->second.starts;
+        h_fl = sd->second.h_flags;
+        need = sd->second.h_need;
+      } else {
+        ORCG_ALLOC_TO(int64_t, dstart, ns + 1);
+        flags = rb_alloc(2, &h_fl);
+        if (!flags) {
+          ORCG_ALLOC_TO(uint64_t, flags, 2);
+          if ((rc = hip_check(ctx, hipMemsetAsync(flags, 0, 16, ctx->stream), "flags memset"))) return fail_ctx(rc);
+        }
+        uint64_t* d_need = rb_alloc(1, &need);
+        if ((rc = launch_exclusive_scan(ctx, dlen, ns, dstart, flags, d_need))) return fail_ctx(rc);
+      }
       StreamBuf& db = c.s[kSlotData];
       c.blob = D->d_stage + db.host_off;
       c.blob_len = db.len;
@@ -2119,6 +2158,8 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   dec_batch[0].clear();
   dec_batch[1].clear();
   dec_done.clear();
+  scan_jobs.clear();
+  scan_done.clear();
   launches.clear();
   const uint64_t nrows = nrows_stripe;
   const int64_t* rg_rows = hs.ngroups ? (const int64_t*)(ds.d_stage + hs.rows_off) : nullptr;
@@ -2153,6 +2194,7 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
       }
       launches.push_back(MultiLaunch{5, mode, d, (uint32_t)g.size(), tiles, 0});
     }
+    for (const ScanJob& j : scan_jobs) launches.push_back(MultiLaunch{6, 0, &j, 1, 0, 0});
     ctx->arena_h = ctx->arena_d = nullptr;
     ctx->arena_cap = 0;
   }

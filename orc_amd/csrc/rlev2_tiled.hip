@@ -2419,23 +2419,41 @@ int plan_rlev2_multi(Ctx* ctx, const RleJob* jobs, uint32_t njobs, std::vector<M
   return ORCG_OK;
 }
 
-// The planned launches, in order; RLEv2 instances (kind 0) run concurrently
-// on side streams when there are several (each is a few hundred to a couple
-// of thousand workgroups of serial walks: together they fill the chip better
-// than one after the other), joined back before anything later.
+// The planned launches, in order. The work before the join runs side by
+// side: the critical RLEv2 instance (the two-pass one, else the one with the
+// most values) on this stream, every other instance on a side lane of its
+// own, and the varint tile counts and RLEv1 segments (kinds 4, 1) on one
+// more lane; then this stream waits for the lanes and runs what reads their
+// outputs (dictionaries, decimals, length scans: kinds 2, 5, 6) itself. The
+// critical path never changes queues: a dependency across HIP queues costs
+// 12-30 us a hop on the MI355X (configs[3] timelines), so the lanes, done
+// long before the critical instance, are the ones waited on, and the
+// post-join kernels follow the critical instance on its own queue.
 int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
-  int ninst = 0;
-  for (const MultiLaunch& m : ls) ninst += m.kind == 0 ? 1 : 0;
-  const bool par = ninst > 1 && side_lanes() > 1 && ctx_lane(ctx, (size_t)ninst - 1) != nullptr;
+  int ninst = 0, crit = -1;
+  bool aux = false;
+  for (size_t i = 0; i < ls.size(); ++i) {
+    const MultiLaunch& m = ls[i];
+    if (m.kind == 1 || m.kind == 4) aux = true;
+    if (m.kind != 0) continue;
+    ++ninst;
+    const bool two = m.spg > 0, ctwo = crit >= 0 && ls[crit].spg > 0;
+    if (crit < 0 || (two && !ctwo) || (two == ctwo && m.values > ls[crit].values)) crit = (int)i;
+  }
+  const int nlanes = (ninst > 0 ? ninst - 1 : 0) + (aux && ninst > 0 ? 1 : 0);
+  const bool par = nlanes > 0 && side_lanes() > 1 && (size_t)nlanes <= side_lanes() &&
+                   ctx_lane(ctx, (size_t)nlanes - 1) != nullptr;
   Ctx* const base = ctx;
-  int li = 0, rc = ORCG_OK;
+  int used = 0, aux_lane = -1, rc = ORCG_OK;
   if (par) rc = hip_check(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork event");
-  // the streams first (RLEv2 instances forked, RLEv1 on this stream
-  // meanwhile), then the join, then what reads their outputs (dictionaries)
+  auto fork = [&](Ctx** c) -> int {  // the next lane, started after the fork point
+    *c = base->lanes[used++];
+    return hip_check(base, hipStreamWaitEvent((*c)->stream, base->ev_fork, 0), "fork wait");
+  };
   bool joined = false;
   auto join = [&]() -> int {
     int r = ORCG_OK;
-    for (int k = 0; par && k < li; ++k) {
+    for (int k = 0; k < used; ++k) {
       int jr = hip_check(base, hipEventRecord(base->ev_join[k], base->lanes[k]->stream), "join event");
       if (!jr) jr = hip_check(base, hipStreamWaitEvent(base->stream, base->ev_join[k], 0), "join wait");
       if (jr && !r) r = jr;
@@ -2443,17 +2461,13 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
     joined = true;
     return r;
   };
-  for (const MultiLaunch& m : ls) {
-    if (rc) break;
-    if ((m.kind == 2 || m.kind == 5) && !joined && (rc = join())) break;
+  for (size_t i = 0; i < ls.size() && !rc; ++i) {
+    const MultiLaunch& m = ls[i];
+    if ((m.kind == 2 || m.kind == 5 || m.kind == 6) && !joined && (rc = join())) break;
     debug_stale("run_multi: before a launch");
     if (m.kind == 0) {
       Ctx* c = base;
-      if (par) {
-        c = base->lanes[li++];
-        rc = hip_check(base, hipStreamWaitEvent(c->stream, base->ev_fork, 0), "fork wait");
-        if (rc) break;
-      }
+      if (par && (int)i != crit && (rc = fork(&c))) break;
       // jobs without a record of their own report into the base's (the
       // lane's own record is the lane's: it frees it)
       unsigned long long* const own = c->d_err;
@@ -2463,21 +2477,38 @@ int run_multi(Ctx* ctx, const std::vector<MultiLaunch>& ls) {
       c->d_err = own;
       if (rc) {
         char b[160];
-        snprintf(b, sizeof b, " (instance %d, %u streams, %llu segments, lane %d)", m.variant, m.njobs,
-                 (unsigned long long)m.grid, par ? li - 1 : -1);
+        snprintf(b, sizeof b, " (instance %d, %u streams, %llu segments%s)", m.variant, m.njobs,
+                 (unsigned long long)m.grid, c == base ? "" : ", side lane");
         base->last_error = c->last_error + b;
       }
-    } else if (m.kind == 1) {
-      rc = launch_rlev1_jobs(base, (const V1SegDesc*)m.d_jobs, m.grid, m.variant);
+    } else if (m.kind == 1 || m.kind == 4) {
+      Ctx* c = base;
+      if (par && !joined) {
+        if (aux_lane < 0) {
+          if ((rc = fork(&c))) break;
+          aux_lane = used - 1;
+        }
+        c = base->lanes[aux_lane];
+      }
+      unsigned long long* const own = c->d_err;
+      c->d_err = base->d_err;
+      if (m.kind == 1) {
+        rc = launch_rlev1_jobs(c, (const V1SegDesc*)m.d_jobs, m.grid, m.variant);
+      } else {
+        const VarintJob& J = *(const VarintJob*)m.d_jobs;
+        uint64_t ntiles = 0;
+        rc = launch_varint_tile_counts(c, J.src, J.len, J.counts, &ntiles);
+        if (!rc) rc = launch_exclusive_scan(c, J.counts, ntiles, J.base, nullptr, J.total);
+      }
+      c->d_err = own;
+      if (rc && c != base) base->last_error = c->last_error;
     } else if (m.kind == 2) {
       rc = launch_dict_jobs(base, (const DictJob*)m.d_jobs, m.njobs, m.grid);
     } else if (m.kind == 5) {
       rc = launch_decimal_jobs(base, (const DecJob*)m.d_jobs, m.njobs, m.grid, m.variant);
-    } else if (m.kind == 4) {
-      const VarintJob& J = *(const VarintJob*)m.d_jobs;
-      uint64_t ntiles = 0;
-      rc = launch_varint_tile_counts(base, J.src, J.len, J.counts, &ntiles);
-      if (!rc) rc = launch_exclusive_scan(base, J.counts, ntiles, J.base, nullptr, J.total);
+    } else if (m.kind == 6) {
+      const ScanJob& J = *(const ScanJob*)m.d_jobs;
+      rc = launch_exclusive_scan(base, J.in, J.n, J.out, J.flags, J.total);
     } else {
       // a pinned single-stream variant: host job (d_jobs is a host pointer)
       const RleJob& J = *(const RleJob*)m.d_jobs;
