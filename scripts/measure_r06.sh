@@ -25,6 +25,9 @@ for s in ${MEAS:-bf_c1 bf_c4 bf_c5 prof_c1 prof_c4 prof_c5}; do
       step $s 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/$s" -o run --output-format csv -- python3 scripts/bench_file.py --workload $w --iters 1 --no-cpu-baseline --check none ;;
     bench) step bench 400 python bench.py ;;
     prof_c2) step prof_c2 400 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/prof_c2" -o run --output-format csv -- python3 bench.py --steps 50 --warmup 100 --no-cpu-baseline --no-verify --copy-inclusive 0 ;;
+    pmc_fetch|pmc_write)
+      c=FETCH_SIZE; [ $s = pmc_write ] && c=WRITE_SIZE
+      step $s 300 timeout -s KILL 280 rocprofv3 --kernel-trace --pmc $c -d "$PWD/$OUT/$s" -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-verify --copy-inclusive 0 ;;
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
   esac
 done
