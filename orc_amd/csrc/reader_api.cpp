@@ -1500,11 +1500,34 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
         std::vector<uint64_t> totals(cur.size(), 0);
         int lr = read_back_lanes(cur, totals.data());
         for (size_t q = 0; q < cur.size() && !lr; ++q) {
-          ctx = cur[q].lane;
+          // a map's keys and values are siblings too: when both launch work
+          // the values go to the next lane of this fork, after what that lane
+          // already holds (C5: the string keys' dictionary chain and the
+          // nullable values' chain, ~190 + ~115 us, ran back to back on the
+          // map's lane while the list's lane idled; a lane of its own would
+          // share one of the process's 4 hardware queues, HIP's default)
+          const std::vector<uint32_t>& subs = footer.types[cur[q].id].subtypes;
+          std::vector<Ctx*> on(subs.size(), cur[q].lane);
+          size_t li = 0;
+          while (li < nl && base->lanes[li] != cur[q].lane) ++li;
+          if (subs.size() == 2 && nl >= 2 && li < nl && device_work(subs[0]) && device_work(subs[1])) {
+            const size_t alt = (li + 1) % nl;
+            Ctx* const L2 = base->lanes[alt];
+            lr = hip_check(base, hipEventRecord(base->ev_join[li], cur[q].lane->stream), "fork event");
+            if (!lr) lr = hip_check(base, hipStreamWaitEvent(L2->stream, base->ev_join[li], 0), "fork wait");
+            if (lr) {
+              lr = fail_ctx(lr);
+            } else {
+              used[alt] = 1;
+              on[1] = L2;
+            }
+          }
           in_lane = true;
           if (fork_rc) err_col = kNoCol;  // an earlier column's inline failure comes first
-          for (uint32_t st : footer.types[cur[q].id].subtypes)
-            if ((lr = decode(st, totals[q], nullptr, totals[q], cur[q].child_rows))) break;
+          for (size_t si = 0; si < subs.size() && !lr; ++si) {
+            ctx = on[si];
+            lr = decode(subs[si], totals[q], nullptr, totals[q], cur[q].child_rows);
+          }
           in_lane = false;
           ctx = base;
         }
