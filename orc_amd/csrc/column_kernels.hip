@@ -877,6 +877,25 @@ int launch_pull(Ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes) {
   return hip_check(ctx, hipGetLastError(), "pull launch");
 }
 
+// Mid-stripe counts the host waits for (list / map totals): one thread
+// copies them into coherent pinned memory, then stores the generation into
+// the flag word with a system-scope release; the host spins on the flag
+// instead of an 8-byte DMA per count and a stream synchronisation (whose
+// interrupt-driven wake-up and the DMA hand-offs cost ~60 us between
+// configs[4]'s decode levels).
+__global__ void publish_kernel(PublishArgs a, uint64_t* __restrict__ dst, uint64_t* flag, uint64_t gen) {
+  if (threadIdx.x != 0) return;
+  for (uint32_t i = 0; i < a.n; ++i)
+    __hip_atomic_store(dst + i, (uint64_t)*a.src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int launch_publish(Ctx* ctx, const PublishArgs& a, uint64_t* d_dst, uint64_t* d_flag, uint64_t gen) {
+  if (a.n > kPublishMax) return set_error(ctx, ORCG_INVALID_ARGUMENT, "too many counts to publish");
+  hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, ctx->stream, a, d_dst, d_flag, gen);
+  return hip_check(ctx, hipGetLastError(), "publish launch");
+}
+
 int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out) {
   if (n == 0) return ORCG_OK;
   const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256 * 32);

@@ -371,6 +371,14 @@ int launch_widen(Ctx* ctx, const void* d_in, int kind, uint64_t n, void* d_out);
 // Host (pinned, device-mapped) -> device copy by a kernel on ctx->stream;
 // both buffers 16-byte aligned, rounded up to whole 16-byte words.
 int launch_pull(Ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes);
+// up to kPublishMax device int64 counts -> d_dst (coherent pinned memory),
+// then *d_flag = gen (system-scope release): the host polls the flag
+constexpr uint32_t kPublishMax = 16;
+struct PublishArgs {
+  const int64_t* src[kPublishMax];
+  uint32_t n;
+};
+int launch_publish(Ctx* ctx, const PublishArgs& a, uint64_t* d_dst, uint64_t* d_flag, uint64_t gen);
 
 // Dispatch on ctx->rlev2_variant.
 inline int launch_rlev2(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_signed,

@@ -450,11 +450,85 @@ struct orcg_reader {
   }
 
   // Mid-stripe reads the host must wait for (list / map totals, union
-  // counts): 8-byte D2H copies into pinned memory (one DMA each; a pageable
-  // destination costs two staging copies), then one stream synchronisation.
+  // counts). Up to kPublishMax counts per stream: publish_kernel writes them
+  // and a generation flag into coherent pinned memory and the host polls the
+  // flag (launch_publish); more: 8-byte D2H copies into pinned memory (one
+  // DMA each), then one stream synchronisation.
+  uint64_t* h_pub = nullptr;  // kPubSlots slots of kPubStride words: counts, then the flag
+  uint64_t* d_pub = nullptr;
+  uint64_t pub_gen = 0;
+  static constexpr size_t kPubSlots = 32, kPubStride = 32;
+  // srcs[i] on stream lanes[i]; 1 = more counts on one stream than a slot
+  // holds (the caller copies them instead)
+  int poll_counts(const std::vector<Ctx*>& lanes, const std::vector<const void*>& srcs, uint64_t* out) {
+    if (!h_pub) {
+      void* h = nullptr;
+      if (hipHostMalloc(&h, kPubSlots * kPubStride * 8, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+      }
+      void* d = nullptr;
+      if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        return 1;
+      }
+      memset(h, 0, kPubSlots * kPubStride * 8);
+      h_pub = (uint64_t*)h;
+      d_pub = (uint64_t*)d;
+    }
+    std::vector<Ctx*> order;  // one slot per stream, in first-use order
+    std::vector<PublishArgs> args;
+    std::vector<std::vector<size_t>> where;
+    for (size_t i = 0; i < srcs.size(); ++i) {
+      size_t g = 0;
+      while (g < order.size() && order[g] != lanes[i]) ++g;
+      if (g == order.size()) {
+        if (g == kPubSlots) return 1;
+        order.push_back(lanes[i]);
+        args.push_back(PublishArgs{});
+        where.emplace_back();
+      }
+      if (args[g].n == kPublishMax) return 1;
+      args[g].src[args[g].n++] = (const int64_t*)srcs[i];
+      where[g].push_back(i);
+    }
+    const uint64_t gen = ++pub_gen;
+    for (size_t g = 0; g < order.size(); ++g) {
+      const int rc = launch_publish(order[g], args[g], d_pub + g * kPubStride, d_pub + g * kPubStride + kPublishMax,
+                                    gen);
+      if (rc) return fail(rc, order[g]->last_error);
+    }
+    for (size_t g = 0; g < order.size(); ++g) {
+      const uint64_t* flag = h_pub + g * kPubStride + kPublishMax;
+      const double t0 = now_s();
+      for (uint32_t spin = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen; ++spin) {
+        if ((spin & 1023) != 0) continue;
+        // a failed stream never sets the flag; a long wait gives the core back
+        const hipError_t q = hipStreamQuery(order[g]->stream);
+        if (q != hipSuccess && q != hipErrorNotReady) {
+          const int rc = hip_check(order[g], q, "publish wait");
+          return fail(rc, order[g]->last_error);
+        }
+        if (q == hipSuccess || now_s() - t0 > 2e-3) {
+          const int rc = hip_check(order[g], hipStreamSynchronize(order[g]->stream), "hipStreamSynchronize");
+          if (rc) return fail(rc, order[g]->last_error);
+          if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != gen)
+            return fail(ORCG_DEVICE_ERROR, "mid-stripe counts were not published");
+          break;
+        }
+      }
+      for (size_t k = 0; k < where[g].size(); ++k) out[where[g][k]] = h_pub[g * kPubStride + k];
+    }
+    return ORCG_OK;
+  }
   uint64_t* h_sync = nullptr;
   size_t sync_cap = 0;
   int read_back(const std::vector<const void*>& src, uint64_t* out) {
+    {
+      const int pr = poll_counts(std::vector<Ctx*>(src.size(), ctx), src, out);
+      if (pr != 1) return pr;
+    }
     if (src.size() > sync_cap) {
       if (h_sync) (void)hipHostFree(h_sync);
       h_sync = nullptr;
@@ -475,6 +549,7 @@ struct orcg_reader {
   }
 
   ~orcg_reader() {
+    if (h_pub) (void)hipHostFree(h_pub);
     slots.clear();
     if (mapped) munmap(mapped, file_len);
     if (h_sync) (void)hipHostFree(h_sync);
@@ -545,6 +620,16 @@ struct orcg_reader {
   // read_back over several side contexts: the D2H copies on each one's
   // stream, then one synchronisation per stream used
   int read_back_lanes(const std::vector<Pending>& ps, uint64_t* out) {
+    {
+      std::vector<Ctx*> lanes(ps.size());
+      std::vector<const void*> srcs(ps.size());
+      for (size_t i = 0; i < ps.size(); ++i) {
+        lanes[i] = ps[i].lane;
+        srcs[i] = ps[i].d_total;
+      }
+      const int pr = poll_counts(lanes, srcs, out);
+      if (pr != 1) return pr;
+    }
     if (ps.size() > sync_cap) {
       if (h_sync) (void)hipHostFree(h_sync);
       h_sync = nullptr;
@@ -1481,25 +1566,44 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
         in_lane = false;
         ctx = base;
       }
-      // the waiting children, level by level (pre-order within a level: the
-      // columns of an earlier sibling come first, so after an inline failure
-      // the earlier siblings' children still run and report theirs first)
+      // the waiting children, level by level. Within a level the subtrees
+      // with the most columns are enqueued first: the host's enqueue of a
+      // level takes longer than a short chain runs (configs[4]: the map's
+      // keys chain, the longest, started ~110 us late behind the list's
+      // items). Errors keep column order: after a failure only columns
+      // before it go on (their device errors would come first), the earliest
+      // column's failure is the one reported, and a level below keeps only
+      // the subtrees before it.
       const int fork_rc = rc;
       const uint32_t fork_col = err_col;
       const std::string fork_msg = last_error;
-      while (!level.empty()) {
+      uint32_t fail_col = fork_rc ? fork_col : kNoCol;
+      int fail_rc = fork_rc;
+      std::string fail_msg = fork_rc ? fork_msg : std::string();
+      int hard = ORCG_OK;  // a failure outside any column's decode: stop
+      std::function<uint32_t(uint32_t)> cols_in = [&](uint32_t t) -> uint32_t {
+        uint32_t k = selected[t] && H->cols[t].supported ? 1u : 0u;
+        for (uint32_t st : footer.types[t].subtypes) k += cols_in(st);
+        return k;
+      };
+      while (!level.empty() && !hard) {
         std::vector<Pending> cur;
         cur.swap(level);
-        if (fork_rc) {
-          // only the children of columns before the failing one
-          size_t keep = 0;
-          while (keep < cur.size() && cur[keep].id < fork_col) ++keep;
-          cur.resize(keep);
-          if (cur.empty()) break;
-        }
+        size_t keep = 0;  // (pre-order: ascending ids)
+        while (keep < cur.size() && cur[keep].id < fail_col) ++keep;
+        cur.resize(keep);
+        if (cur.empty()) break;
         std::vector<uint64_t> totals(cur.size(), 0);
-        int lr = read_back_lanes(cur, totals.data());
-        for (size_t q = 0; q < cur.size() && !lr; ++q) {
+        if ((hard = read_back_lanes(cur, totals.data()))) break;
+        std::vector<uint32_t> weight(cur.size());
+        std::vector<size_t> ord(cur.size());
+        for (size_t q = 0; q < cur.size(); ++q) {
+          weight[q] = cols_in(cur[q].id);
+          ord[q] = q;
+        }
+        std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return weight[x] > weight[y]; });
+        for (size_t q : ord) {
+          if (cur[q].id >= fail_col) continue;  // after an earlier failure
           // a map's keys and values are siblings too: when both launch work
           // the values go to the next lane of this fork, after what that lane
           // already holds (C5: the string keys' dictionary chain and the
@@ -1513,33 +1617,42 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
           if (subs.size() == 2 && nl >= 2 && li < nl && device_work(subs[0]) && device_work(subs[1])) {
             const size_t alt = (li + 1) % nl;
             Ctx* const L2 = base->lanes[alt];
-            lr = hip_check(base, hipEventRecord(base->ev_join[li], cur[q].lane->stream), "fork event");
-            if (!lr) lr = hip_check(base, hipStreamWaitEvent(L2->stream, base->ev_join[li], 0), "fork wait");
-            if (lr) {
-              lr = fail_ctx(lr);
-            } else {
-              used[alt] = 1;
-              on[1] = L2;
+            hard = hip_check(base, hipEventRecord(base->ev_join[li], cur[q].lane->stream), "fork event");
+            if (!hard) hard = hip_check(base, hipStreamWaitEvent(L2->stream, base->ev_join[li], 0), "fork wait");
+            if (hard) {
+              hard = fail_ctx(hard);
+              break;
             }
+            used[alt] = 1;
+            on[1] = L2;
           }
           in_lane = true;
-          if (fork_rc) err_col = kNoCol;  // an earlier column's inline failure comes first
+          err_col = kNoCol;
+          int lr = ORCG_OK;
           for (size_t si = 0; si < subs.size() && !lr; ++si) {
             ctx = on[si];
             lr = decode(subs[si], totals[q], nullptr, totals[q], cur[q].child_rows);
           }
           in_lane = false;
           ctx = base;
-        }
-        if (lr) {
-          rc = lr;
-          break;
+          if (lr) {
+            const uint32_t ec = err_col != kNoCol ? err_col : cur[q].id;
+            if (ec < fail_col) {
+              fail_col = ec;
+              fail_rc = lr;
+              fail_msg = last_error;
+            }
+          }
         }
       }
       pending = nullptr;
-      if (fork_rc && rc == fork_rc && err_col == kNoCol) {
-        err_col = fork_col;
-        last_error = fork_msg;
+      if (hard) {
+        rc = hard;
+      } else if (fail_rc) {
+        rc = fail_rc;
+        err_col = fail_col;
+        last_error = fail_msg;
+        ctx->last_error = fail_msg;
       }
       for (unsigned l = 0; l < nl; ++l) {
         if (!used[l]) continue;
