@@ -687,6 +687,10 @@ struct orcg_reader {
   };
   std::vector<DictJob> dict_batch;
   std::unordered_map<uint32_t, DictDone> dict_done;
+  // dictionaries of columns the batch cannot take whole (nullable, under a
+  // list / map): their entry offsets and summary only, from the same launch
+  std::unordered_map<uint32_t, DictDone> dict_pre;
+  int collect_dicts(uint32_t id);
   // varint decimal DATA streams whose tile counts + scan run with the batch
   // (before its join): their tile bases and value-count slots by column
   std::deque<VarintJob> varint_jobs;
@@ -1047,12 +1051,51 @@ int orcg_reader::queue_scan(uint32_t id, uint64_t n) {
   return ORCG_OK;
 }
 
+// Dictionaries below a column collect() does not descend into (a nullable
+// column's subtree, a list's or map's children): a dictionary's size is in
+// the stripe footer, so its LENGTH stream and entry offsets join the batch
+// instead of being decoded after the parent's counts come back mid-stripe
+// (configs[4]: the map keys' dictionary took three dependent launches on an
+// idle GPU after the element counts were published, each blocking the host
+// ~60-80 us, profiles/r06/inv/hip_api_c5_548c478.txt). LoadStringDictionary
+// reads it whole whatever the rows (DictionaryLoader.cc:43-97).
+int orcg_reader::collect_dicts(uint32_t id) {
+  Col& c = H->cols[id];
+  if (!selected[id] || !c.supported) return ORCG_OK;
+  const uint32_t k = c.kind;
+  if (is_string_kind(k) && (c.encoding == kDictionary || c.encoding == kDictionaryV2)) {
+    const uint64_t D_ = c.dict_size;
+    if (D_ == 0 || D_ > kDictLds || !c.s[kSlotLength].present) return ORCG_OK;
+    int rc = queue_stream(id, kSlotLength, false, D_, false);
+    if (rc) return rc;
+    const auto li = batched.find((uint64_t)id * 8 + kSlotLength);
+    if (li == batched.end() || li->second.second != D_) return ORCG_OK;
+    DictJob j{};
+    j.lengths = li->second.first;
+    j.dict_size = D_;
+    ORCG_ALLOC_TO(int64_t, j.offsets, D_ + 1);
+    const uint64_t* h_summary = nullptr;
+    j.summary = rb_alloc(2, &h_summary);
+    if (!j.summary) return ORCG_OK;
+    j.n = 0;  // offsets and summary only: decode() gathers the rows
+    j.err = D->d_errs + id;
+    dict_batch.push_back(j);
+    dict_pre[id] = DictDone{j.offsets, h_summary, nullptr, nullptr, nullptr};
+    return ORCG_OK;
+  }
+  for (uint32_t st : footer.types[id].subtypes) {
+    const int rc = collect_dicts(st);
+    if (rc) return rc;
+  }
+  return ORCG_OK;
+}
+
 // The streams decode() will read with host-known counts, in its order
 // (same slots, signedness and counts as decode()'s int_stream calls).
 int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
   Col& c = H->cols[id];
   if (!selected[id] || !c.supported) return ORCG_OK;
-  if (c.s[kSlotPresent].present) return ORCG_OK;  // its counts come from the device
+  if (c.s[kSlotPresent].present) return collect_dicts(id);  // its counts come from the device
   cur_rows = rg_rows;
   cur_n = n;
   cur_in_nn = nullptr;
@@ -1083,6 +1126,8 @@ int orcg_reader::collect(uint32_t id, uint64_t n, const int64_t* rg_rows) {
     }
   } else if (k == ORCG_TYPE_LIST || k == ORCG_TYPE_MAP) {
     rc = queue_stream(id, kSlotLength, false, n, false);
+    for (uint32_t st : footer.types[id].subtypes)
+      if (!rc) rc = collect_dicts(st);
   } else if (k == ORCG_TYPE_STRUCT) {
     for (uint32_t st : footer.types[id].subtypes)
       if ((rc = collect(st, n, rg_rows))) break;
@@ -1386,24 +1431,33 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
       const std::string cid = std::to_string(id);
       if (dict_size > 0 && !has_len)
         return fail(ORCG_PARSE_ERROR, "LENGTH stream not found in StringDictionaryColumn for column " + cid);
-      int64_t* dlen;
-      ORCG_ALLOC(int64_t, doff, dict_size + 1);
-      if ((rc = int_stream(c, kSlotLength, false, dict_size, &dlen))) return rc;
-      const uint64_t* h_sum = nullptr;
-      uint64_t* summary = rb_alloc(2, &h_sum);  // blob bytes, negative-length flag
-      if (!summary) ORCG_ALLOC_TO(uint64_t, summary, 2);
-      if (dict_size <= 65536) {
-        // offsets, blob size and the negative-length check in one launch
-        if ((rc = launch_dict_offsets(ctx, dlen, dict_size, doff, summary))) return fail_ctx(rc);
+      int64_t* doff;
+      const uint64_t* h;
+      const auto pre = dict_pre.find(id);
+      if (pre != dict_pre.end()) {
+        // offsets and summary from the stripe's dictionary launch (collect_dicts)
+        doff = pre->second.offsets;
+        h = pre->second.h_summary;
       } else {
-        if ((rc = launch_flag_negative(ctx, dlen, dict_size, summary + 1))) return fail_ctx(rc);
-        if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
-        if ((rc = hip_check(ctx, hipMemcpyAsync(summary, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream),
-                            "copy")))
-          return fail_ctx(rc);
+        int64_t* dlen;
+        ORCG_ALLOC_TO(int64_t, doff, dict_size + 1);
+        if ((rc = int_stream(c, kSlotLength, false, dict_size, &dlen))) return rc;
+        const uint64_t* h_sum = nullptr;
+        uint64_t* summary = rb_alloc(2, &h_sum);  // blob bytes, negative-length flag
+        if (!summary) ORCG_ALLOC_TO(uint64_t, summary, 2);
+        if (dict_size <= 65536) {
+          // offsets, blob size and the negative-length check in one launch
+          if ((rc = launch_dict_offsets(ctx, dlen, dict_size, doff, summary))) return fail_ctx(rc);
+        } else {
+          if ((rc = launch_flag_negative(ctx, dlen, dict_size, summary + 1))) return fail_ctx(rc);
+          if ((rc = launch_exclusive_scan(ctx, dlen, dict_size, doff))) return fail_ctx(rc);
+          if ((rc = hip_check(ctx, hipMemcpyAsync(summary, doff + dict_size, 8, hipMemcpyDeviceToDevice, ctx->stream),
+                              "copy")))
+            return fail_ctx(rc);
+        }
+        h = defer(summary, 2);
+        if (!h) return fail(ORCG_DEVICE_ERROR, "D2H of the dictionary size failed");
       }
-      const uint64_t* h = defer(summary, 2);
-      if (!h) return fail(ORCG_DEVICE_ERROR, "D2H of the dictionary size failed");
       StreamBuf& db = c.s[kSlotDict];
       Col* cp = &c;
       const bool db_present = db.present;
@@ -2289,6 +2343,7 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   batched.clear();
   dict_batch.clear();
   dict_done.clear();
+  dict_pre.clear();
   varint_jobs.clear();
   varint_pre.clear();
   dec_batch[0].clear();
