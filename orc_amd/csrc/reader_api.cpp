@@ -549,6 +549,7 @@ struct orcg_reader {
   }
 
   ~orcg_reader() {
+    if (ev_pre) (void)hipEventDestroy(ev_pre);
     if (h_pub) (void)hipHostFree(h_pub);
     slots.clear();
     if (mapped) munmap(mapped, file_len);
@@ -691,6 +692,10 @@ struct orcg_reader {
   // list / map): their entry offsets and summary only, from the same launch
   std::unordered_map<uint32_t, DictDone> dict_pre;
   int collect_dicts(uint32_t id);
+  // a batch of such dictionaries only runs on side lane 0 (issue()); the
+  // gathers reading its offsets and the stripe's read-back wait on ev_pre
+  hipEvent_t ev_pre = nullptr;
+  bool pre_on_lane = false;
   // varint decimal DATA streams whose tile counts + scan run with the batch
   // (before its join): their tile bases and value-count slots by column
   std::deque<VarintJob> varint_jobs;
@@ -1438,6 +1443,8 @@ int orcg_reader::decode(uint32_t id, uint64_t n, const uint8_t* in_nn, uint64_t 
         // offsets and summary from the stripe's dictionary launch (collect_dicts)
         doff = pre->second.offsets;
         h = pre->second.h_summary;
+        if (pre_on_lane && (rc = hip_check(ctx, hipStreamWaitEvent(ctx->stream, ev_pre, 0), "dictionary batch wait")))
+          return fail_ctx(rc);
       } else {
         int64_t* dlen;
         ORCG_ALLOC_TO(int64_t, doff, dict_size + 1);
@@ -2064,6 +2071,19 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& 
     }, ri_bytes, 16u << 10);  // row indexes: ~16 KB of (compressed) entries per thread
     if (any) hs.ngroups = G;
   }
+  // columns whose value streams decode in a launch of their own, never in the
+  // stripe's multi-stream batch (collect() stops at a PRESENT stream and at a
+  // list's or map's children): a column with nulls, or one below a list, a
+  // map or a column with nulls (configs[4]'s map keys)
+  std::vector<uint8_t> alone(nt, 0);
+  for (size_t i = 0; i < nt; ++i) {
+    const Col& c = hs.cols[i];
+    const bool down = alone[i] || c.s[kSlotPresent].present || c.kind == ORCG_TYPE_LIST || c.kind == ORCG_TYPE_MAP;
+    if (c.s[kSlotPresent].present) alone[i] = 1;
+    if (down)
+      for (uint32_t st : footer.types[i].subtypes)
+        if (st < nt && st > i) alone[st] = 1;  // (pre-order ids: children after parents)
+  }
   // host run plans (header walks only) for every RLE stream, in parallel
   std::vector<StreamBuf*> rle;
   std::vector<int> rle_kind;  // 0 byte RLE, 1 RLEv1, 2 RLEv2
@@ -2097,13 +2117,15 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& 
       // chases run headers ~2 KB apart through memory (~45 ns a run, 0.9 ms
       // for a 42 MB stream), which lands on the host-bound critical path
       //
-      // A nullable column's RLEv2 stream of long runs (its first runs
-      // average >= 96 bytes: DIRECT / PATCHED_BASE runs of hundreds of
-      // values) gets a host plan with 8 KB segments too: a child column's row
-      // group holds ~40,000 values in several serial window passes of one
-      // workgroup (C5's list items and map values: 260 workgroups per
-      // stream), while the host walk costs ~45 ns a run, a few thousand runs
-      // a stripe. Columns without nulls keep the row index: their streams
+      // An RLEv2 stream of long runs (its first runs average >= 96 bytes:
+      // DIRECT / PATCHED_BASE runs of hundreds of values) in a launch of its
+      // own (`alone`: a nullable column, or one below a list, a map or a
+      // nullable column) gets a host plan with 8 KB segments too: a child
+      // column's row group holds ~40,000 values in several serial window
+      // passes of one workgroup (C5's list items, map keys and map values:
+      // 260 workgroups per stream; the keys' launch took 135 us a stripe),
+      // while the host walk costs ~45 ns a run, a few thousand runs a
+      // stripe. Batched columns keep the row index: their streams
       // share one multi-stream launch with the short-run streams, whose
       // latency sets its length, and the extra host walk lands on the
       // host-bound wall (C4: device 3.46 -> 3.64 ms, host plans 3.4 -> 7.8 ms
@@ -2118,8 +2140,7 @@ int orcg_reader::prepare(uint64_t s, HostStage& hs, const std::vector<uint8_t>& 
           // (rlev1_kernel's narrow instance) -- the host walk is ~1 ns a byte
         } else if (kind == 0) {
           if (per_group <= (2u << 10)) continue;
-        } else if (kind == 2 && c.s[kSlotPresent].present && per_group > (8u << 10) &&
-                   long_runs(hs.h + sb.host_off, sb.len)) {
+        } else if (kind == 2 && alone[i] && per_group > (8u << 10) && long_runs(hs.h + sb.host_off, sb.len)) {
           fine = true;
         } else {
           continue;
@@ -2403,9 +2424,29 @@ void orcg_reader::issue(HostStage& hs, DevSlot& ds, Flight& fl) {
   if (urc && !rc) rc = fail_ctx(urc);
   if (fl.ev_split && hipEventRecord(fl.ev_up1, ctx->stream) != hipSuccess) fl.ev_split = false;
   fl.t1 = now_s();
-  if (!rc && !launches.empty() && (rc = timed(0, [&]() -> int { return run_multi(ctx, launches); })))
+  // A batch of nested or nullable columns' dictionaries only (collect_dicts;
+  // configs[4]'s map keys): nothing reads its offsets before the fork's next
+  // level, so it runs on side lane 0 beside the stripe's first decodes, not
+  // ahead of them on the base stream (4 launches, ~45 us of a C5 stripe)
+  pre_on_lane = false;
+  Ctx* pre_lane = nullptr;
+  if (!rc && !launches.empty() && batched.size() == dict_pre.size() && dict_done.empty() && scan_jobs.empty() &&
+      dec_batch[0].empty() && dec_batch[1].empty() && varint_jobs.empty() && side_lanes() > 1 &&
+      (ev_pre || hipEventCreateWithFlags(&ev_pre, hipEventDisableTiming) == hipSuccess))
+    pre_lane = ctx_lane(ctx, 0);
+  if (!rc && pre_lane) {
+    rc = hip_check(ctx, hipEventRecord(ctx->ev_fork, ctx->stream), "fork event");
+    if (!rc) rc = hip_check(ctx, hipStreamWaitEvent(pre_lane->stream, ctx->ev_fork, 0), "fork wait");
+    if (!rc && (rc = run_multi(pre_lane, launches))) ctx->last_error = pre_lane->last_error;
+    if (!rc) rc = hip_check(ctx, hipEventRecord(ev_pre, pre_lane->stream), "dictionary batch event");
+    if (rc) rc = fail_ctx(rc);
+    pre_on_lane = !rc;
+  } else if (!rc && !launches.empty() && (rc = timed(0, [&]() -> int { return run_multi(ctx, launches); }))) {
     rc = fail_ctx(rc);
+  }
   if (!rc) rc = decode(0, nrows, nullptr, nrows, rg_rows);
+  if (pre_on_lane && hipStreamWaitEvent(ctx->stream, ev_pre, 0) != hipSuccess && !rc)
+    rc = fail(ORCG_DEVICE_ERROR, "dictionary batch wait failed");
   batched_streams += batched.size();
   fl.rc = rc;
   fl.err_col = err_col;
