@@ -2315,8 +2315,17 @@ int launch_rlev2_tiled(Ctx* ctx, const uint8_t* d_src, uint64_t src_len, int is_
                        int dst_bytes, const uint64_t* d_count) {
   int variant = ctx->rlev2_variant;
   if (variant == 0) {
-    variant = default_variant(src_len, positions_mode ? nsegs * rows_per_group : nvalues);
+    const uint64_t est = positions_mode ? nsegs * rows_per_group : nvalues;
+    variant = default_variant(src_len, est);
     if (variant == 6) variant = union_variant(ctx, nsegs);
+    // more than 8.1 stream bytes a value is more than any 64-bit payload:
+    // the excess is run headers, i.e. runs of ~20 values or fewer of wide
+    // values (short DIRECT / PATCHED_BASE), whose expansion the two-pass
+    // union balances by values at any segment count (sweep short DIRECT
+    // 64-bit, 10,000 segments: 217 GB/s in the serial walk, 270 in one union
+    // pass, 379 in two; profiles/r06/sweep_shortdirect_64_548c478.jsonl).
+    // 512-value W=64 runs (configs[1]) are 8.004 B/value: the serial walk.
+    else if (variant == 2 && 10 * src_len > 81 * est) variant = 6;
   }
   return launch_tiled(ctx, variant, d_src, src_len, is_signed, d_segtab, nsegs, positions_mode, rows_per_group,
                       value_begin, nvalues, d_dst, dst_bytes, nullptr, 0, d_count);

@@ -279,6 +279,44 @@ def test_wide_short_runs_vs_oracle():
     ctx.set_rlev2_variant(0)
 
 
+@pytest.mark.parametrize("signed", [True, False])
+def test_short_wide_direct_default_routing_vs_oracle(signed):
+    """Short DIRECT runs (1-12 values) of full 64-bit values: more than 8.1
+    stream bytes a value, which variant 0 sends to the two-pass union instead
+    of the serial walk (launch_rlev2_tiled). Row-index positions (one row
+    group, many, and a stride that cuts runs) and value windows, against the
+    oracle's RleDecoderV2 restatement."""
+    import torch
+
+    import orc_amd
+
+    rng = np.random.default_rng(64 + int(signed))
+    lens = rng.integers(1, 13, size=40_000).astype(np.uint32)
+    n = int(lens.sum())
+    lo, hi = (-(1 << 63), (1 << 63) - 1) if signed else (0, (1 << 64) - 1)
+    v = rng.integers(lo, hi, size=n, endpoint=True, dtype=np.int64 if signed else np.uint64).view(np.int64)
+    kinds = np.ones(lens.size, dtype=np.uint8)
+    want = oracle.rlev2_decode(orc_amd.encode_runs(v, signed, kinds, lens)[0].tobytes(), n, signed)
+    np.testing.assert_array_equal(want, v)
+    ctx = orc_amd.default_context(0)
+    ctx.set_rlev2_variant(0)
+    for stride in (10_000, 777, 1 << 30):
+        data, pos = _encode_with_positions(orc_amd, v, signed, kinds, lens, stride)
+        assert 10 * data.size > 81 * n  # the rule's side of 8.1 B/value
+        d_src = torch.from_numpy(data).cuda()
+        d_pos = torch.from_numpy(pos.view(np.int64)).cuda()
+        out = torch.full((n,), -7, dtype=torch.int64, device="cuda")
+        orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, n, signed, out)
+        ctx.synchronize()
+        got = out.cpu().numpy()
+        assert np.array_equal(got, want), "stride %d: first mismatch at %d" % (stride, int(np.argmax(got != want)))
+        for a, b in [(12345, 54321), (n - 7, n)]:
+            o = torch.full((b - a,), -7, dtype=torch.int64, device="cuda")
+            orc_amd.decode_positions_device(ctx, d_src, d_pos, stride, b - a, signed, o, value_begin=a)
+            ctx.synchronize()
+            np.testing.assert_array_equal(o.cpu().numpy(), want[a:b])
+
+
 @pytest.mark.parametrize("bits", [7, 33, 64])
 @pytest.mark.parametrize("signed", [True, False])
 def test_value_parallel_expansion_vs_oracle(bits, signed):
