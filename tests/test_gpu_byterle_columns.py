@@ -266,3 +266,27 @@ def test_truncated_stream_reports_first_bad_group(orc):
         with pytest.raises(orc.ParseError) as ge:
             gd.next(len(raw))
         assert "bad read in nextBuffer" in str(ge.value) and str(we.value) in str(ge.value)
+
+
+@pytest.mark.parametrize("n,p_null", [(1, 0.0), (4095, 0.5), (4097, 1.0), (1_000_003, 0.0), (9_000_011, 0.37),
+                                      (9_000_011, 0.999)])
+def test_scatter_lookback_sizes(orc, n, p_null):
+    """The placement's single launch: each 4,096-row tile's first dense index
+    from a decoupled look-back over the tiles' non-null counts (one tile,
+    tile edges, all-null tiles, ~2,200 tiles), repeated launches on one
+    context (a new look-back epoch each), against numpy's placement."""
+    import torch
+
+    rng = np.random.default_rng(n)
+    nn = (rng.random(n) >= p_null).astype(np.uint8)
+    k = int(nn.sum())
+    dense = rng.integers(-(1 << 62), 1 << 62, size=k).astype(np.int64)
+    ctx = orc.default_context(0)
+    d_dense, d_nn = torch.from_numpy(dense).cuda(), torch.from_numpy(nn).cuda()
+    want = np.full(n, -9, dtype=np.int64)
+    want[nn == 1] = dense
+    for _ in range(3):
+        out = torch.full((n,), 7, dtype=torch.int64, device="cuda")
+        orc.scatter_not_null_device(ctx, d_dense, d_nn, out, fill=-9)
+        ctx.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), want)
