@@ -282,7 +282,9 @@ def test_scatter_lookback_sizes(orc, n, p_null):
     k = int(nn.sum())
     dense = rng.integers(-(1 << 62), 1 << 62, size=k).astype(np.int64)
     ctx = orc.default_context(0)
-    d_dense, d_nn = torch.from_numpy(dense).cuda(), torch.from_numpy(nn).cuda()
+    # (an all-null column still hands the C ABI a dense buffer: it checks for one)
+    d_dense = torch.from_numpy(dense if k else np.zeros(1, dtype=np.int64)).cuda()
+    d_nn = torch.from_numpy(nn).cuda()
     want = np.full(n, -9, dtype=np.int64)
     want[nn == 1] = dense
     for _ in range(3):
