@@ -1,7 +1,9 @@
 #!/bin/bash
-# A/B: a C5 map's values on a spare side lane (liborcgpu.so) vs the fork's
-# next lane (liborcgpu_base.so, the tree before), interleaved on one box,
-# after the reader GPU tests on the new library.
+# A/B of a reader change on configs[4]: the tree's library (liborcgpu.so)
+# against liborcgpu_base.so (a copy of the build before the change),
+# interleaved on one box, after the reader GPU tests on the new library.
+# Used for the spare-lane, values-first and fine-stream instance A/Bs
+# (profiles/r06/inv/ab_*_c5.jsonl).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
